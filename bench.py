@@ -1,0 +1,271 @@
+"""BICOS hot-path benchmark (driver contract: one JSON line on rank 0).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2]
+  torchrun --nproc-per-node N bench.py --gpus N ...      (one process per GPU, RCCL)
+
+A step = one full BICOS::match of the configured synthetic stereo frame
+(transform x2 -> Hamming search -> NXC agree [-> subpixel]) with the planar
+stacks already resident in HBM. With N > 1 the frame is split into N row bands
+(one per GPU, strong scaling) and the disparity + correlation bands are gathered
+to rank 0 with ONE RCCL gather per step, inside the timed region.
+
+Extra keys on the JSON line:
+  roofline      the dominant kernel (the Hamming search), timed live with HIP
+                events on the stream it runs on; algorithmic INT32 lane-ops per
+                launch / average launch time vs the VALU peak (the search is
+                VALU-bound, not HBM- or MFMA-bound: DESIGN.md s5). `hbm` holds the
+                HBM-bound stages (transform, agree) against the 8 TB/s peak.
+  cpu_baseline  the C oracle (oracle/bicos_oracle.c, -march=x86-64-v3) on this
+                host's cores, rank 0 at N=1 only, over a bounded row sample.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+# MI355X (gfx950) peaks, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters":
+# 256 CUs x 4 SIMD-32 x 2.4 GHz -> 128 int32 lane-ops/clk/CU = 78.6 T lane-op/s
+VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12
+HBM_PEAK_GBS = 8000.0
+
+CONFIGS = {
+    # BASELINE.json configs; "cfg2" is the one the headline metric is quoted on
+    "cfg1": dict(n=8, H=480, W=640, dtype="u8", cfg=dict(nxcorr_threshold=0.9),
+                 desc="8x2 stack @ 640x480 u8, LIMITED 32-bit, nxcorr 0.9"),
+    "cfg2": dict(n=33, H=1536, W=2048, dtype="u8", cfg=dict(nxcorr_threshold=0.96),
+                 desc="33x2 stack @ 2048x1536 u8, LIMITED 128-bit (4n-7=125 bits), nxcorr 0.96"),
+    "cfg3": dict(n=33, H=1536, W=2048, dtype="u8",
+                 cfg=dict(nxcorr_threshold=0.96, min_variance=2.0, subpixel_step=0.1),
+                 desc="33x2 @ 2048x1536 u8, 128-bit, nxcorr 0.96, min-variance 2.0, subpixel 0.1"),
+    "cfg4": dict(n=40, H=1536, W=2048, dtype="u8",
+                 cfg=dict(nxcorr_threshold=0.96, variant=1, max_lr_diff=1),
+                 desc="40x2 @ 2048x1536 u8, LIMITED 256-bit, LR-consistency max_lr_diff 1, nxcorr 0.96"),
+    "cfg5": dict(n=33, H=2160, W=3840, dtype="u8", cfg=dict(nxcorr_threshold=0.96),
+                 desc="33x2 @ 3840x2160 u8, 128-bit, nxcorr 0.96"),
+}
+
+
+def search_ops(rows: int, W: int, words: int, cfg: dict) -> float:
+    """Algorithmic INT32 lane-ops of the search kernel launches of one match:
+    per (col0, col1) pair: `words` xor + `words` bcnt + key pack + min (+ med3 with
+    NoDuplicates)  = 2w+3 (NoDuplicates) / 2w+2 per direction (Consistency)."""
+    if cfg.get("variant", 0) == 1:
+        per = 2 * words + (3 if cfg.get("no_dupes") else 2)
+        return 2.0 * rows * W * W * per
+    return float(rows) * W * W * (2 * words + 3)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="strong: one frame split in row bands; weak: a full frame per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0,
+                    help="target wall time of the CPU baseline sample")
+    ap.add_argument("--kernel-reps", type=int, default=10)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from libbicos_amd import _lib, device
+    from libbicos_amd.distributed import band_height, band_rows
+    from libbicos_amd.synthetic import stereo_stack
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but WORLD_SIZE=%d (launch N>1 with torchrun)" % (args.gpus, world))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    C = CONFIGS[args.config]
+    n, H, W = C["n"], C["H"], C["W"]
+    mcfg = device.MatchConfig(**C["cfg"])
+    words = device.descriptor_words(n, mcfg.mode)
+    if args.scaling == "strong":
+        b, e = band_rows(H, world, rank)
+    else:
+        b, e = 0, H
+    rows = e - b
+
+    # synthetic stacks of this rank's band, generated on the host once, resident in HBM
+    L, R = stereo_stack(n, H, W, np.uint8, row_begin=b, row_end=e)
+    s0 = torch.from_numpy(L).to(dev)
+    s1 = torch.from_numpy(R).to(dev)
+    del L, R
+    eng = device.Engine(local)
+    has_corr = mcfg.nxcorr_threshold is not None
+    out = torch.empty((rows, W), dtype=torch.float32 if has_corr else torch.int16, device=dev)
+    corr = torch.empty((rows, W), dtype=torch.float32, device=dev) if has_corr else None
+
+    gather = world > 1 and args.scaling == "strong"
+    if gather:
+        hb = band_height(H, world)
+        # one packed buffer -> one RCCL gather per step (disparity + corrmap bands)
+        planes = 2 if has_corr else 1
+        send = torch.zeros((planes, hb, W), dtype=torch.float32, device=dev)
+        recv = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+
+    def step():
+        eng.match(s0, s1, mcfg, out=out, corrmap=corr)
+        if gather:
+            send[0, :rows].copy_(out if has_corr else out.float())
+            if has_corr:
+                send[1, :rows].copy_(corr)
+            dist.gather(send, recv, dst=0)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    frames_px = H * W * (world if args.scaling == "weak" else 1)
+    value = frames_px * args.steps / elapsed / 1e6
+    ms_per_step = elapsed / args.steps * 1e3
+
+    # ---- dominant kernel, timed live: HIP events on the stream the search runs on
+    st = torch.cuda.current_stream(dev)
+    d0 = eng.transform(s0, mcfg.mode, words)
+    d1 = eng.transform(s1, mcfg.mode, words)
+    raw = torch.empty((rows, W), dtype=torch.int16, device=dev)
+    flags = (2 | (1 if mcfg.no_dupes else 0)) if mcfg.variant == 1 else 1
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw)  # warm
+    ev[0].record(st)
+    for _ in range(args.kernel_reps):
+        eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw)
+    ev[1].record(st)
+    for _ in range(args.kernel_reps):
+        eng.transform(s0, mcfg.mode, words, out=d0)
+    ev[2].record(st)
+    ev[3].record(st)
+    for _ in range(args.kernel_reps):
+        eng.agree(raw, s0, s1, 0.96)
+    ev[4].record(st)
+    torch.cuda.synchronize(dev)
+    t_search = ev[0].elapsed_time(ev[1]) / args.kernel_reps * 1e-3
+    t_tf = ev[1].elapsed_time(ev[2]) / args.kernel_reps * 1e-3
+    t_agree = ev[3].elapsed_time(ev[4]) / args.kernel_reps * 1e-3
+    ops = search_ops(rows, W, words, C["cfg"])
+    achieved = ops / t_search / 1e12
+    # HBM stages, algorithmic bytes: transform reads n B/px and writes 4w B/px (one stack);
+    # agree reads the int16 raw disparity + 2n B per valid px, writes 8 B/px (disp + corr)
+    tf_bytes = rows * W * (n + 4 * words)
+    valid = float((raw != -32768).float().mean().item())
+    ag_bytes = rows * W * (2 + 8) + rows * W * valid * 2 * n
+
+    roof = {
+        "kernel": "search_kernel<%d words>" % words,
+        "bound": "valu",
+        "achieved": round(achieved, 2),
+        "peak": round(VALU_PEAK_TOPS, 2),
+        "unit": "Tops/s (int32 lane-ops)",
+        "frac": round(achieved / VALU_PEAK_TOPS, 4),
+        "traffic": None,
+        "ops_per_launch": ops,
+        "ms_per_launch": round(t_search * 1e3, 4),
+        "hbm": {
+            "transform_GBps": round(tf_bytes / t_tf / 1e9, 1),
+            "transform_frac": round(tf_bytes / t_tf / 1e9 / HBM_PEAK_GBS, 4),
+            "transform_ms": round(t_tf * 1e3, 4),
+            "agree_GBps": round(ag_bytes / t_agree / 1e9, 1),
+            "agree_frac": round(ag_bytes / t_agree / 1e9 / HBM_PEAK_GBS, 4),
+            "agree_ms": round(t_agree * 1e3, 4),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+        },
+    }
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(C, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "disparity Mpix/s + ms/match, 33x2 stack @ 2048x1536, 1/2/4/8 MI355X",
+            "value": round(value, 2),
+            "unit": "Mpix/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": args.scaling,
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (splitmix64 planted-disparity stereo, seed 0x600DF00D)",
+            "config": {
+                "workload": "%s: %s" % (args.config, C["desc"]),
+                "n_images": n, "rows": H, "cols": W, "descriptor_bits": 32 * words,
+                "parallelism": ("row-bands x%d + RCCL gather" % world) if gather else
+                               ("replicas x%d" % world if world > 1 else "single GPU"),
+                "match_config": C["cfg"],
+            },
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(C, seconds):
+    """The C oracle on this host's cores over a bounded row sample of the same frame."""
+    import numpy as np
+    from libbicos_amd.synthetic import stereo_stack
+    from oracle import oracle
+
+    n, H, W = C["n"], C["H"], C["W"]
+    cores = min(os.cpu_count() or 1, 16)
+    ocfg = oracle.OracleConfig(**C["cfg"])
+    probe = max(cores, 8)
+    L, R = stereo_stack(n, H, W, np.uint8, row_begin=0, row_end=probe)
+    t = time.perf_counter()
+    oracle.match(L, R, ocfg, nthreads=cores, variant="v3")
+    per_row = (time.perf_counter() - t) / probe
+    rows = int(max(probe, min(H, seconds / max(per_row, 1e-9))))
+    rows = max(cores, rows // cores * cores)
+    L, R = stereo_stack(n, H, W, np.uint8, row_begin=0, row_end=rows)
+    t = time.perf_counter()
+    oracle.match(L, R, ocfg, nthreads=cores, variant="v3")
+    el = time.perf_counter() - t
+    return {
+        "value": round(rows * W / el / 1e6, 4),
+        "unit": "Mpix/s",
+        "cores": cores,
+        "kind": "port",
+        "sample": "%d of %d rows (x %d cols, n=%d) full match, %.1f s, oracle -O3 -march=x86-64-v3 "
+                  "-ffp-contract=off, %d threads" % (rows, H, W, n, el, cores),
+        "ms_per_match_extrapolated": round(el / rows * H * 1e3, 1),
+    }
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,154 @@
+/*
+ * bicos_c.h -- C-ABI of libbicos_amd.so, the MI355X (gfx950) BICOS engine.
+ *
+ * Two layers, both plain C (pointers, sizes, ints; no C++ or torch types):
+ *
+ * 1. The reference's ctypes ABI, symbol for symbol (drop-in for pybicos_c.so):
+ *      BicosConfig / BicosResult          reference src/pybicos_c.cpp:30-53
+ *      BICOS_CreateDefaultConfig           reference src/pybicos_c.cpp:92-108
+ *      BICOS_FreeConfig                    reference src/pybicos_c.cpp:111-113
+ *      BICOS_FreeResult                    reference src/pybicos_c.cpp:116-118
+ *      BICOS_Match                         reference src/pybicos_c.cpp:131-200
+ *      BICOS_InvalidDisparityFloat/Int16   reference src/pybicos_c.cpp:203-209
+ *    Host buffers in, malloc'd host copies out -- exactly the reference contract,
+ *    with three documented fixes:
+ *      - BicosConfig ALWAYS carries `precision` (the reference's Python wrapper,
+ *        pybicos/__init__.py:41-51, always lays it out; the reference's CPU build
+ *        omitted it and silently shifted the struct);
+ *      - BICOS_FreeResult frees the data buffers too (the reference leaked them);
+ *      - every exception is caught at the boundary (NULL result), not only
+ *        BICOS::Exception; bicos_last_error() says why.
+ *
+ * 2. The device-resident hot path (bicos_hip_*): device pointers to planar image
+ *    stacks already in HBM, results written to caller-provided device buffers,
+ *    asynchronous on the caller's HIP stream. This is the entry point the
+ *    reference's CUDA build exposes through BICOS::match(GpuMat...) with a
+ *    cv::cuda::Stream (reference include/match.hpp:31-41, src/impl/cuda.cu:465-524),
+ *    restated without OpenCV types.
+ *
+ * Error convention: int-returning functions return BICOS_OK (0) or a negative
+ * BICOS_E_* code; bicos_last_error() returns a thread-local message.
+ */
+#ifndef BICOS_C_H
+#define BICOS_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* OpenCV type codes used across the ABI (CV_MAKETYPE(depth, 1)) */
+#define BICOS_CV_8U 0
+#define BICOS_CV_16U 2
+#define BICOS_CV_16S 3
+#define BICOS_CV_32F 5
+#define BICOS_CV_64F 6
+
+/* reference src/pybicos_c.cpp:30-41 (with `precision` unconditionally present) */
+typedef struct {
+    float nxcorr_threshold; /* < 0: keep the default 0.5 (reference :59-61) */
+    float subpixel_step;    /* < 0: no subpixel refinement */
+    float min_variance;     /* < 0: no minimum variance */
+    int mode;               /* 0 = LIMITED, 1 = FULL */
+    int precision;          /* 0 = SINGLE, 1 = DOUBLE */
+    int variant_type;       /* 0 = NoDuplicates, 1 = Consistency */
+    int max_lr_diff;        /* Consistency only */
+    int no_dupes;           /* Consistency only */
+} BicosConfig;
+
+/* reference src/pybicos_c.cpp:44-53 */
+typedef struct {
+    void* disparity_data;
+    int disparity_rows;
+    int disparity_cols;
+    int disparity_type;
+    void* corrmap_data;
+    int corrmap_rows;
+    int corrmap_cols;
+    int corrmap_type;
+} BicosResult;
+
+BicosConfig* BICOS_CreateDefaultConfig(void);
+void BICOS_FreeConfig(BicosConfig* config);
+void BICOS_FreeResult(BicosResult* result);
+BicosResult* BICOS_Match(void** stack0_data, int* stack0_rows, int* stack0_cols, int* stack0_types,
+                         int stack0_size, void** stack1_data, int* stack1_rows, int* stack1_cols,
+                         int* stack1_types, int stack1_size, BicosConfig* config);
+float BICOS_InvalidDisparityFloat(void);
+int16_t BICOS_InvalidDisparityInt16(void);
+
+/* ------------------------------------------------------------------ errors */
+enum {
+    BICOS_OK = 0,
+    BICOS_E_ARG = -1,       /* invalid argument (BICOS::Exception in the reference) */
+    BICOS_E_BITS = -2,      /* stacks need > 256 descriptor bits (std::invalid_argument) */
+    BICOS_E_HIP = -3,       /* HIP runtime error */
+    BICOS_E_INTERNAL = -4
+};
+const char* bicos_last_error(void);
+
+/* --------------------------------------------------- device-resident API */
+
+/* Opaque per-device engine: owns a workspace (descriptor buffers, temporaries)
+ * that grows on demand and is reused across calls. Not thread-safe per handle;
+ * use one handle per host thread / stream. */
+typedef struct bicos_engine bicos_engine;
+
+int bicos_engine_create(int device, bicos_engine** out);
+void bicos_engine_destroy(bicos_engine* e);
+
+/* Descriptor width in 32-bit words for n images in `mode` (reference dispatch
+ * src/impl/cpu.cpp:122-156); BICOS_E_BITS when more than 256 bits are needed. */
+int bicos_descriptor_words(int n, int mode);
+
+/* Output element type BICOS_Match / bicos_match_device produce for a config:
+ * BICOS_CV_16S without a correlation threshold, else BICOS_CV_32F
+ * (BICOS_CV_64F corrmap for precision DOUBLE). */
+int bicos_output_type(const BicosConfig* cfg, int has_nxcorr);
+
+/*
+ * Full match on device-resident planar stacks.
+ *   stack0/stack1 : n planes each; element (t, y, x) at
+ *                   base[t*plane_pitch + y*row_pitch + x], u8 (depth 1) or u16 (depth 2)
+ *   has_nxcorr    : 0 disables the NXC stage (Config::nxcorr_threshold = nullopt, only
+ *                   reachable from C++ in the reference); disparity is then int16
+ *   disparity     : device, rows*cols dense, int16 or float32 per bicos_output_type
+ *   corrmap       : device, rows*cols dense float32 (float64 for DOUBLE), or NULL
+ *   stream        : hipStream_t (NULL = default stream); the call only enqueues work
+ */
+int bicos_match_device(bicos_engine* e, const void* stack0, const void* stack1, int n, int rows,
+                       int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                       const BicosConfig* cfg, int has_nxcorr, void* disparity, void* corrmap,
+                       void* stream);
+
+/* Stage entry points (tests, benchmarks, custom pipelines). Same conventions.
+ * desc buffers: rows x desc_pitch uint32 with desc_pitch = bicos_desc_pitch(cols, words). */
+size_t bicos_desc_pitch(int cols, int words);
+int bicos_transform_device(const void* stack, int n, int rows, int cols, size_t row_pitch,
+                           size_t plane_pitch, int depth, int mode, int words, uint32_t* desc,
+                           void* stream);
+/* flags: 1 = NODUPES, 2 = CONSISTENCY (reference impl/common.hpp:46-47). Consistency needs
+ * the engine's workspace; out is int16 rows x cols (dense). */
+int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* desc1, int rows,
+                        int cols, int words, int flags, int max_lr_diff, int16_t* out,
+                        void* stream);
+/* agree: raw int16 disparity -> float32 disparity (+ corrmap); minvar already x n */
+int bicos_agree_device(const int16_t* raw, const void* stack0, const void* stack1, int n, int rows,
+                       int cols, size_t row_pitch, size_t plane_pitch, int depth, float threshold,
+                       int has_minvar, float minvar_scaled, float* out, float* corrmap,
+                       void* stream);
+int bicos_subpixel_device(const int16_t* raw, const void* stack0, const void* stack1, int n,
+                          int rows, int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                          float threshold, float step, int has_minvar, float minvar_scaled,
+                          float* out, float* corrmap, void* stream);
+
+/* Build identification (arch, flags) for reports. */
+const char* bicos_build_info(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BICOS_C_H */

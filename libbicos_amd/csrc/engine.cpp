@@ -1,0 +1,550 @@
+// engine.cpp -- host orchestration of the gfx950 BICOS hot path + the C++ API.
+//
+//   bicos_impl::match_device   <- reference match_impl (src/impl/cpu.cpp:35-98)
+//   BICOS::match               <- reference BICOS::match (src/lib.cpp:31-49) and the
+//                                 backend entry impl::cpu::match (src/impl/cpu.cpp:100-159)
+#include "engine.hpp"
+
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <sstream>
+#include <vector>
+
+#include "../../include/bicos/match.hpp"
+
+namespace bicos_impl {
+
+namespace {
+thread_local std::string g_last_error;
+
+constexpr size_t ALIGN = 256;
+size_t align_up(size_t x) { return (x + ALIGN - 1) / ALIGN * ALIGN; }
+}  // namespace
+
+void set_error(int code, const std::string& msg) {
+    (void)code;
+    g_last_error = msg;
+}
+
+int fail(int code, const std::string& msg) {
+    set_error(code, msg);
+    return code;
+}
+
+int check_hip(hipError_t e, const char* what) {
+    if (e == hipSuccess) return BICOS_OK;
+    std::ostringstream os;
+    os << what << ": " << hipGetErrorName(e) << " (" << hipGetErrorString(e) << ")";
+    return fail(BICOS_E_HIP, os.str());
+}
+
+const char* last_error() { return g_last_error.c_str(); }
+
+int reserve(void*& buf, size_t& have, size_t bytes, int device) {
+    if (bytes <= have && buf) return BICOS_OK;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    if (cur != device) (void)hipSetDevice(device);
+    if (buf) {
+        // in-flight work may still read the old buffer
+        (void)hipDeviceSynchronize();
+        (void)hipFree(buf);
+        buf = nullptr;
+        have = 0;
+    }
+    const size_t want = bytes + bytes / 8;  // headroom for slightly larger calls
+    int rc = check_hip(hipMalloc(&buf, want), "hipMalloc(workspace)");
+    if (cur != device) (void)hipSetDevice(cur);
+    if (rc != BICOS_OK) {
+        buf = nullptr;
+        return rc;
+    }
+    have = want;
+    return BICOS_OK;
+}
+
+// reference src/impl/cpu.cpp:122-156
+int descriptor_words(int n, int mode) {
+    const long bits = mode ? (long)n * n - 2L * n + 3 : 4L * n - 7;
+    if (bits <= 32) return 1;
+    if (bits <= 64) return 2;
+    if (bits <= 128) return 4;
+    if (bits <= 256) return 8;
+    return BICOS_E_BITS;
+}
+
+static int required_bits(int n, int mode) { return mode ? n * n - 2 * n + 3 : 4 * n - 7; }
+
+int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int rows, int cols,
+                 size_t row_pitch, size_t plane_pitch, int depth, const BicosConfig& cfg,
+                 bool has_nxcorr, float threshold, void* disp, void* corr, hipStream_t st) {
+    if (!e) return fail(BICOS_E_ARG, "null engine");
+    if (n < 2) return fail(BICOS_E_ARG, "need at least two images");
+    if (depth != 1 && depth != 2)
+        return fail(BICOS_E_ARG, "bad input depths, only CV_8UC1 and CV_16UC1 are supported");
+    if (rows < 0 || cols < 0) return fail(BICOS_E_ARG, "negative image size");
+    if (cols > 32767)
+        return fail(BICOS_E_ARG, "image width exceeds the int16 disparity range (32767)");
+    const int mode = cfg.mode == 0 ? 0 : 1;
+    const int words = descriptor_words(n, mode);
+    if (words < 0) {
+        std::ostringstream os;
+        os << "input stacks too large, would require " << required_bits(n, mode) << " bits";
+        return fail(BICOS_E_BITS, os.str());
+    }
+    const bool has_step = has_nxcorr && cfg.subpixel_step >= 0;
+    if (has_step && !(cfg.subpixel_step > 0 && std::isfinite(cfg.subpixel_step)))
+        return fail(BICOS_E_ARG, "subpixel_step must be a positive finite number");
+    if (rows == 0 || cols == 0) return BICOS_OK;
+    if (!s0 || !s1 || !disp) return fail(BICOS_E_ARG, "null buffer");
+    if (row_pitch < (size_t)cols || plane_pitch < (size_t)rows * row_pitch)
+        return fail(BICOS_E_ARG, "row/plane pitch smaller than the image");
+
+    const bool consistency = cfg.variant_type != 0;
+    const bool nodupes = consistency ? cfg.no_dupes != 0 : true;
+    const bool dbl = cfg.precision != 0;
+
+    // workspace: desc0 | desc1 | raw int16 | fwd | rev
+    const size_t dpitch = bicos_desc_pitch(cols, words);
+    const size_t desc_bytes = align_up((size_t)rows * dpitch * 4);
+    const size_t map16 = align_up((size_t)rows * cols * 2);
+    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) + (consistency ? 2 * map16 : 0);
+    int rc = reserve(e->ws, e->ws_bytes, need, e->device);
+    if (rc) return rc;
+    char* p = (char*)e->ws;
+    uint32_t* d0 = (uint32_t*)p;
+    p += desc_bytes;
+    uint32_t* d1 = (uint32_t*)p;
+    p += desc_bytes;
+    int16_t* raw = has_nxcorr ? (int16_t*)p : (int16_t*)disp;
+    if (has_nxcorr) p += map16;
+    int16_t* fwd = consistency ? (int16_t*)p : nullptr;
+    int16_t* rev = consistency ? (int16_t*)(p + map16) : nullptr;
+
+    // 1. descriptor_transform, both stacks in one launch (cpu.cpp:50-59)
+    bicos_hip::TransformArgs ta{s0, s1, d0, d1, n, rows, cols, row_pitch, plane_pitch, dpitch};
+    rc = check_hip(bicos_hip::launch_transform(ta, depth, mode, words, st), "transform launch");
+    if (rc) return rc;
+
+    // 2. bicos search (cpu.cpp:68-75)
+    const bicos_hip::SearchGeometry g = bicos_hip::search_geometry(rows, cols, words, e->max_lds);
+    if (!consistency) {
+        bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
+        rc = check_hip(bicos_hip::launch_search(sa, g, words, true, st), "search launch");
+        if (rc) return rc;
+    } else {
+        bicos_hip::SearchArgs fa{d0, d1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
+        rc = check_hip(bicos_hip::launch_search(fa, g, words, nodupes, st), "search launch");
+        if (rc) return rc;
+        bicos_hip::SearchArgs ra{d1, d0, rev, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
+        rc = check_hip(bicos_hip::launch_search(ra, g, words, nodupes, st), "reverse search launch");
+        if (rc) return rc;
+        bicos_hip::ConsistencyArgs ca{fwd, rev, raw, rows, cols, (size_t)cols, cfg.max_lr_diff};
+        rc = check_hip(bicos_hip::launch_consistency(ca, st), "consistency launch");
+        if (rc) return rc;
+    }
+    if (!has_nxcorr) return BICOS_OK;
+
+    // 3. agree / agree_subpixel (cpu.cpp:77-95)
+    bicos_hip::AgreeArgs aa{};
+    aa.raw = raw;
+    aa.raw_pitch = (size_t)cols;
+    aa.stack0 = s0;
+    aa.stack1 = s1;
+    aa.n = n;
+    aa.rows = rows;
+    aa.cols = cols;
+    aa.row_pitch = row_pitch;
+    aa.plane_pitch = plane_pitch;
+    aa.threshold = threshold;
+    aa.step = has_step ? cfg.subpixel_step : 0.f;
+    aa.has_minvar = cfg.min_variance >= 0;
+    aa.minvar = aa.has_minvar ? cfg.min_variance * (float)n : 0.f;  // cpu.cpp:127
+    aa.out = disp;
+    aa.out_f32 = 1;
+    aa.corrmap = corr;
+    if (has_step)
+        rc = check_hip(bicos_hip::launch_subpixel(aa, depth, dbl, st), "subpixel launch");
+    else
+        rc = check_hip(bicos_hip::launch_agree(aa, depth, dbl, st), "agree launch");
+    return rc;
+}
+
+bicos_engine* default_engine(int device) {
+    static std::mutex m;
+    static std::map<int, bicos_engine*> engines;
+    std::lock_guard<std::mutex> g(m);
+    auto it = engines.find(device);
+    if (it != engines.end()) return it->second;
+    bicos_engine* e = nullptr;
+    if (bicos_engine_create(device, &e) != BICOS_OK) return nullptr;
+    engines[device] = e;
+    return e;
+}
+
+}  // namespace bicos_impl
+
+// ------------------------------------------------------------- C-ABI: engine
+
+using namespace bicos_impl;
+
+extern "C" {
+
+const char* bicos_last_error(void) { return bicos_impl::last_error(); }
+
+int bicos_engine_create(int device, bicos_engine** out) {
+    if (!out) return fail(BICOS_E_ARG, "null out");
+    *out = nullptr;
+    int count = 0;
+    int rc = check_hip(hipGetDeviceCount(&count), "hipGetDeviceCount");
+    if (rc) return rc;
+    if (device < 0 || device >= count) return fail(BICOS_E_ARG, "no such HIP device");
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device);
+    auto* e = new bicos_engine();
+    e->device = device;
+    int lds = 0;
+    if (hipDeviceGetAttribute(&lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) ==
+            hipSuccess &&
+        lds > 0) {
+        // keep the per-workgroup right-row stage <= 64 KiB so >= 2 workgroups fit per CU
+        e->max_lds = lds < 64 * 1024 ? lds : 64 * 1024;
+    }
+    rc = check_hip(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking), "hipStreamCreate");
+    (void)hipSetDevice(cur);
+    if (rc) {
+        delete e;
+        return rc;
+    }
+    *out = e;
+    return BICOS_OK;
+}
+
+void bicos_engine_destroy(bicos_engine* e) {
+    if (!e) return;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(e->device);
+    (void)hipDeviceSynchronize();
+    if (e->ws) (void)hipFree(e->ws);
+    if (e->stage) (void)hipFree(e->stage);
+    if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+    (void)hipSetDevice(cur);
+    delete e;
+}
+
+int bicos_descriptor_words(int n, int mode) {
+    if (n < 2) return fail(BICOS_E_ARG, "need at least two images");
+    const int w = descriptor_words(n, mode ? 1 : 0);
+    if (w < 0) return fail(BICOS_E_BITS, "input stacks too large");
+    return w;
+}
+
+int bicos_output_type(const BicosConfig* cfg, int has_nxcorr) {
+    (void)cfg;
+    return has_nxcorr ? BICOS_CV_32F : BICOS_CV_16S;
+}
+
+size_t bicos_desc_pitch(int cols, int words) {
+    return ((size_t)cols * words + 3) / 4 * 4;
+}
+
+int bicos_match_device(bicos_engine* e, const void* stack0, const void* stack1, int n, int rows,
+                       int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                       const BicosConfig* cfg, int has_nxcorr, void* disparity, void* corrmap,
+                       void* stream) {
+    if (!cfg) return fail(BICOS_E_ARG, "null config");
+    try {
+        // reference src/pybicos_c.cpp:59-61: a negative threshold keeps the default 0.5
+        const float thr = cfg->nxcorr_threshold >= 0 ? cfg->nxcorr_threshold : 0.5f;
+        return match_device(e, stack0, stack1, n, rows, cols, row_pitch, plane_pitch, depth, *cfg,
+                            has_nxcorr != 0, thr, disparity, corrmap, (hipStream_t)stream);
+    } catch (const std::exception& ex) {
+        return fail(BICOS_E_INTERNAL, ex.what());
+    } catch (...) {
+        return fail(BICOS_E_INTERNAL, "unknown exception");
+    }
+}
+
+int bicos_transform_device(const void* stack, int n, int rows, int cols, size_t row_pitch,
+                           size_t plane_pitch, int depth, int mode, int words, uint32_t* desc,
+                           void* stream) {
+    if (n < 2) return fail(BICOS_E_ARG, "need at least two images");
+    if (depth != 1 && depth != 2) return fail(BICOS_E_ARG, "bad input depth");
+    if (words != 1 && words != 2 && words != 4 && words != 8)
+        return fail(BICOS_E_ARG, "words must be 1, 2, 4 or 8");
+    const int need = descriptor_words(n, mode ? 1 : 0);
+    if (need < 0 || need > words) return fail(BICOS_E_BITS, "descriptor too narrow for n");
+    bicos_hip::TransformArgs ta{stack, nullptr, desc, nullptr, n, rows, cols,
+                                row_pitch, plane_pitch, bicos_desc_pitch(cols, words)};
+    return check_hip(bicos_hip::launch_transform(ta, depth, mode ? 1 : 0, words, (hipStream_t)stream),
+                     "transform launch");
+}
+
+int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* desc1, int rows,
+                        int cols, int words, int flags, int max_lr_diff, int16_t* out,
+                        void* stream) {
+    if (words != 1 && words != 2 && words != 4 && words != 8)
+        return fail(BICOS_E_ARG, "words must be 1, 2, 4 or 8");
+    if (cols > 32767) return fail(BICOS_E_ARG, "image width exceeds 32767");
+    if (rows <= 0 || cols <= 0) return BICOS_OK;
+    hipStream_t st = (hipStream_t)stream;
+    const size_t dpitch = bicos_desc_pitch(cols, words);
+    const bool nodupes = (flags & 1) != 0;
+    const int max_lds = e ? e->max_lds : 64 * 1024;
+    const bicos_hip::SearchGeometry g = bicos_hip::search_geometry(rows, cols, words, max_lds);
+    if (!(flags & 2)) {
+        bicos_hip::SearchArgs sa{desc0, desc1, out, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
+        return check_hip(bicos_hip::launch_search(sa, g, words, nodupes, st), "search launch");
+    }
+    if (!e) return fail(BICOS_E_ARG, "consistency search needs an engine workspace");
+    const size_t map16 = align_up((size_t)rows * cols * 2);
+    int rc = reserve(e->ws, e->ws_bytes, 2 * map16, e->device);
+    if (rc) return rc;
+    int16_t* fwd = (int16_t*)e->ws;
+    int16_t* rev = (int16_t*)((char*)e->ws + map16);
+    bicos_hip::SearchArgs fa{desc0, desc1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
+    rc = check_hip(bicos_hip::launch_search(fa, g, words, nodupes, st), "search launch");
+    if (rc) return rc;
+    bicos_hip::SearchArgs ra{desc1, desc0, rev, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
+    rc = check_hip(bicos_hip::launch_search(ra, g, words, nodupes, st), "reverse search launch");
+    if (rc) return rc;
+    bicos_hip::ConsistencyArgs ca{fwd, rev, out, rows, cols, (size_t)cols, max_lr_diff};
+    return check_hip(bicos_hip::launch_consistency(ca, st), "consistency launch");
+}
+
+static int agree_common(bool sub, const int16_t* raw, const void* stack0, const void* stack1,
+                        int n, int rows, int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                        float threshold, float step, int has_minvar, float minvar_scaled,
+                        float* out, float* corrmap, void* stream) {
+    if (n < 2) return fail(BICOS_E_ARG, "need at least two images");
+    if (n > 65 && sub) return fail(BICOS_E_ARG, "subpixel supports n <= 65");
+    if (depth != 1 && depth != 2) return fail(BICOS_E_ARG, "bad input depth");
+    if (sub && !(step > 0 && std::isfinite(step)))
+        return fail(BICOS_E_ARG, "subpixel_step must be a positive finite number");
+    bicos_hip::AgreeArgs aa{};
+    aa.raw = raw;
+    aa.raw_pitch = (size_t)cols;
+    aa.stack0 = stack0;
+    aa.stack1 = stack1;
+    aa.n = n;
+    aa.rows = rows;
+    aa.cols = cols;
+    aa.row_pitch = row_pitch;
+    aa.plane_pitch = plane_pitch;
+    aa.threshold = threshold;
+    aa.step = step;
+    aa.has_minvar = has_minvar;
+    aa.minvar = minvar_scaled;
+    aa.out = out;
+    aa.out_f32 = 1;
+    aa.corrmap = corrmap;
+    hipStream_t st = (hipStream_t)stream;
+    return sub ? check_hip(bicos_hip::launch_subpixel(aa, depth, false, st), "subpixel launch")
+               : check_hip(bicos_hip::launch_agree(aa, depth, false, st), "agree launch");
+}
+
+int bicos_agree_device(const int16_t* raw, const void* stack0, const void* stack1, int n, int rows,
+                       int cols, size_t row_pitch, size_t plane_pitch, int depth, float threshold,
+                       int has_minvar, float minvar_scaled, float* out, float* corrmap,
+                       void* stream) {
+    return agree_common(false, raw, stack0, stack1, n, rows, cols, row_pitch, plane_pitch, depth,
+                        threshold, 0.f, has_minvar, minvar_scaled, out, corrmap, stream);
+}
+
+int bicos_subpixel_device(const int16_t* raw, const void* stack0, const void* stack1, int n,
+                          int rows, int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                          float threshold, float step, int has_minvar, float minvar_scaled,
+                          float* out, float* corrmap, void* stream) {
+    return agree_common(true, raw, stack0, stack1, n, rows, cols, row_pitch, plane_pitch, depth,
+                        threshold, step, has_minvar, minvar_scaled, out, corrmap, stream);
+}
+
+const char* bicos_build_info(void) {
+    return "libbicos_amd: gfx950 HIP kernels (transform, LDS-broadcast popcount/argmin search, "
+           "NXC agree/subpixel), -O3 -ffp-contract=off";
+}
+
+}  // extern "C"
+
+// --------------------------------------------------------------- C++ API
+
+namespace BICOS {
+
+size_t Image::elem_size(int type) {
+    switch (type) {
+        case U8: return 1;
+        case U16:
+        case S16: return 2;
+        case F32: return 4;
+        case F64: return 8;
+    }
+    throw Exception("unsupported image type " + std::to_string(type));
+}
+
+Image::Image(int rows, int cols, int type, void* data, size_t step, Memory mem)
+    : _data(data), _rows(rows), _cols(cols), _type(type), _mem(mem) {
+    _step = step ? step : (size_t)cols * elem_size(type);
+}
+
+void Image::create(int rows, int cols, int type, Memory mem) {
+    if (_owner && _rows == rows && _cols == cols && _type == type && _mem == mem) return;
+    const size_t step = (size_t)cols * elem_size(type);
+    const size_t bytes = step * rows;
+    void* p = nullptr;
+    if (mem == Memory::Host) {
+        p = std::malloc(bytes ? bytes : 1);
+        if (!p) throw Exception("out of host memory");
+        _owner = std::shared_ptr<void>(p, [](void* q) { std::free(q); });
+    } else {
+        if (hipMalloc(&p, bytes ? bytes : 1) != hipSuccess) throw Exception("hipMalloc failed");
+        _owner = std::shared_ptr<void>(p, [](void* q) { (void)hipFree(q); });
+    }
+    _data = p;
+    _rows = rows;
+    _cols = cols;
+    _type = type;
+    _step = step;
+    _mem = mem;
+}
+
+Image Image::download() const {
+    if (_mem == Memory::Host) return *this;
+    Image h = allocate(_rows, _cols, _type, Memory::Host);
+    if (!empty() &&
+        hipMemcpy2D(h._data, h._step, _data, _step, (size_t)_cols * elemSize(), _rows,
+                    hipMemcpyDeviceToHost) != hipSuccess)
+        throw Exception("download failed");
+    return h;
+}
+
+static void throw_rc(int rc) {
+    if (rc != BICOS_OK) throw Exception(bicos_impl::last_error());
+}
+
+// reference src/impl/cpu.cpp:100-159 (validation, dispatch) + src/lib.cpp:31-49
+void match(const std::vector<Image>& stack0, const std::vector<Image>& stack1, Image& disparity,
+           Config cfg, Image* corrmap, hipStream_t stream) {
+    const size_t n = stack0.size();
+    if (n < 2) throw Exception("need at least two images");
+    if (stack1.size() != n) throw Exception("stacks differ in length");
+    const Image& f = stack0.front();
+    if (f.type() != U8 && f.type() != U16)
+        throw Exception("bad input depths, only CV_8UC1 and CV_16UC1 are supported");
+    const Memory mem = f.memory();
+    for (const auto* s : {&stack0, &stack1})
+        for (const Image& im : *s)
+            if (im.rows() != f.rows() || im.cols() != f.cols() || im.type() != f.type() ||
+                im.memory() != mem)
+                throw Exception("all images must share size, type and memory");
+    const int rows = f.rows(), cols = f.cols();
+    const int depth = (int)f.elemSize();
+
+    BicosConfig c{};
+    const bool has_nxcorr = cfg.nxcorr_threshold.has_value();
+    c.nxcorr_threshold = has_nxcorr ? *cfg.nxcorr_threshold : 0.5f;
+    c.subpixel_step = cfg.subpixel_step ? *cfg.subpixel_step : -1.f;
+    c.min_variance = cfg.min_variance ? *cfg.min_variance : -1.f;
+    c.mode = cfg.mode == TransformMode::FULL ? 1 : 0;
+    c.precision = cfg.precision == Precision::DOUBLE ? 1 : 0;
+    if (auto* cons = std::get_if<Variant::Consistency>(&cfg.variant)) {
+        c.variant_type = 1;
+        c.max_lr_diff = cons->max_lr_diff;
+        c.no_dupes = cons->no_dupes;
+    }
+    if (cfg.subpixel_step && !(*cfg.subpixel_step > 0))
+        throw Exception("subpixel_step must be a positive finite number");
+    if (cfg.min_variance && *cfg.min_variance < 0) c.min_variance = -1.f;
+
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    bicos_engine* e = bicos_impl::default_engine(dev);
+    if (!e) throw Exception(bicos_impl::last_error());
+    std::lock_guard<std::mutex> g(e->lock);
+    hipStream_t st = mem == Memory::Host ? e->own_stream : stream;
+
+    // the planar device stacks the kernels read
+    const size_t elem = (size_t)depth;
+    const void* s0 = nullptr;
+    const void* s1 = nullptr;
+    size_t row_pitch = (size_t)cols, plane_pitch = (size_t)rows * cols;
+    auto uniform = [&](const std::vector<Image>& s, size_t& rp, size_t& pp) {
+        // zero-copy when the images already form one planar buffer with a common pitch
+        if (s[0].step() % elem) return false;
+        rp = s[0].step() / elem;
+        const char* b = (const char*)s[0].data();
+        if (n < 2) return false;
+        const ptrdiff_t d = (const char*)s[1].data() - b;
+        if (d <= 0 || d % (ptrdiff_t)elem) return false;
+        for (size_t t = 0; t < n; ++t)
+            if (s[t].step() != s[0].step() || (const char*)s[t].data() != b + (ptrdiff_t)t * d)
+                return false;
+        pp = (size_t)d / elem;
+        return pp >= (size_t)rows * rp;
+    };
+    size_t rp0 = 0, pp0 = 0, rp1 = 0, pp1 = 0;
+    const size_t plane_bytes = (size_t)rows * cols * elem;
+    if (mem == Memory::Device && uniform(stack0, rp0, pp0) && uniform(stack1, rp1, pp1) &&
+        rp0 == rp1 && pp0 == pp1) {
+        s0 = stack0[0].data();
+        s1 = stack1[0].data();
+        row_pitch = rp0;
+        plane_pitch = pp0;
+    } else if (rows > 0 && cols > 0) {
+        throw_rc(reserve(e->stage, e->stage_bytes, 2 * n * plane_bytes, e->device));
+        char* dst = (char*)e->stage;
+        const hipMemcpyKind kind =
+            mem == Memory::Host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+        for (size_t t = 0; t < n; ++t) {
+            throw_rc(check_hip(hipMemcpy2DAsync(dst + t * plane_bytes, cols * elem,
+                                                stack0[t].data(), stack0[t].step(), cols * elem,
+                                                rows, kind, st),
+                               "stack upload"));
+            throw_rc(check_hip(hipMemcpy2DAsync(dst + (n + t) * plane_bytes, cols * elem,
+                                                stack1[t].data(), stack1[t].step(), cols * elem,
+                                                rows, kind, st),
+                               "stack upload"));
+        }
+        s0 = dst;
+        s1 = dst + n * plane_bytes;
+    }
+
+    const int dtype = has_nxcorr ? F32 : S16;
+    const bool dbl = c.precision != 0;
+    Image ddisp, dcorr;
+    const bool want_corr = corrmap && has_nxcorr;
+    if (mem == Memory::Device) {
+        disparity.create(rows, cols, dtype, Memory::Device);
+        if (want_corr) corrmap->create(rows, cols, dbl ? F64 : F32, Memory::Device);
+        ddisp = disparity;
+        if (want_corr) dcorr = *corrmap;
+    } else {
+        ddisp.create(rows, cols, dtype, Memory::Device);
+        if (want_corr) dcorr.create(rows, cols, dbl ? F64 : F32, Memory::Device);
+    }
+    throw_rc(bicos_impl::match_device(e, s0, s1, (int)n, rows, cols, row_pitch, plane_pitch, depth,
+                                      c, has_nxcorr, c.nxcorr_threshold, ddisp.data(),
+                                      want_corr ? dcorr.data() : nullptr,
+                                      st));
+    if (mem == Memory::Host) {
+        disparity.create(rows, cols, dtype, Memory::Host);
+        if (want_corr) corrmap->create(rows, cols, dbl ? F64 : F32, Memory::Host);
+        if (rows > 0 && cols > 0) {
+            throw_rc(check_hip(hipMemcpyAsync(disparity.data(), ddisp.data(),
+                                              (size_t)rows * cols * Image::elem_size(dtype),
+                                              hipMemcpyDeviceToHost, st),
+                               "download"));
+            if (want_corr)
+                throw_rc(check_hip(hipMemcpyAsync(corrmap->data(), dcorr.data(),
+                                                  (size_t)rows * cols * (dbl ? 8 : 4),
+                                                  hipMemcpyDeviceToHost, st),
+                                   "download"));
+        }
+        throw_rc(check_hip(hipStreamSynchronize(st), "hipStreamSynchronize"));
+    }
+}
+
+}  // namespace BICOS

@@ -1,0 +1,74 @@
+// kernels.hpp -- launch interface of the gfx950 BICOS kernels (kernels.hip).
+// Plain structs of device pointers and sizes; every launcher is asynchronous on `st`.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace bicos_hip {
+
+struct TransformArgs {
+    const void* stack0;     // planar [n][rows][row_pitch] u8/u16
+    const void* stack1;     // second stack (or nullptr: transform stack0 only)
+    uint32_t* desc0;        // [rows][desc_pitch] uint32
+    uint32_t* desc1;
+    int n, rows, cols;
+    size_t row_pitch;       // elements
+    size_t plane_pitch;     // elements
+    size_t desc_pitch;      // uint32 words per descriptor row
+};
+
+struct SearchArgs {
+    const uint32_t* desc0;  // the side whose pixels are matched (col0)
+    const uint32_t* desc1;  // the side that is searched (col1)
+    int16_t* out;
+    int rows, cols;
+    size_t desc_pitch;      // uint32 words
+    size_t out_pitch;       // int16 elements
+    int out_mode;           // 0: disparity col0-best (INVALID -32768), 1: best index (-1)
+    int chunk;              // set by launch_search
+    int tiles_per_row;      // set by launch_search
+};
+
+struct SearchGeometry {
+    int chunk;              // col1 columns per LDS fill
+    int waves;              // waves per workgroup
+    int R;                  // col0 per lane
+    int tiles_per_row;
+};
+
+struct ConsistencyArgs {
+    const int16_t* fwd;     // [rows][cols] best col1 or -1
+    const int16_t* rev;     // [rows][cols] best col0 of the reverse search or -1
+    int16_t* out;
+    int rows, cols;
+    size_t out_pitch;
+    int max_lr_diff;
+};
+
+struct AgreeArgs {
+    const int16_t* raw;     // integer disparity from the search
+    size_t raw_pitch;
+    const void* stack0;
+    const void* stack1;
+    int n, rows, cols;
+    size_t row_pitch, plane_pitch;
+    float threshold;
+    float step;             // subpixel only
+    int has_minvar;
+    float minvar;           // already scaled by n (reference cpu.cpp:127)
+    void* out;              // dense [rows][cols]
+    int out_f32;            // agree: 1 -> float32 output, 0 -> int16 in place semantics
+    void* corrmap;          // dense [rows][cols] float (double for DOUBLE) or nullptr
+};
+
+hipError_t launch_transform(const TransformArgs& a, int depth, int mode, int words, hipStream_t st);
+SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes);
+hipError_t launch_search(SearchArgs a, const SearchGeometry& g, int words, bool nodupes,
+                         hipStream_t st);
+hipError_t launch_consistency(const ConsistencyArgs& a, hipStream_t st);
+hipError_t launch_agree(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
+hipError_t launch_subpixel(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
+
+}  // namespace bicos_hip

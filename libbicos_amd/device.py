@@ -1,0 +1,197 @@
+"""Device-resident BICOS on MI355X: torch tensors in HBM -> libbicos_amd C-ABI.
+
+This is the reference CUDA build's entry point (BICOS::match on cv::cuda::GpuMat
+with a cv::cuda::Stream, reference include/match.hpp:31-41) for Python callers
+that keep their stacks on the GPU. torch supplies device memory and the stream;
+every kernel is hand-written HIP in libbicos_amd.so. There is no CPU fallback.
+
+Stacks are planar tensors [n, rows, cols] (uint8, or uint16 held in an int16 /
+uint16 tensor with depth=2), possibly a row band of a larger frame.
+"""
+from __future__ import annotations
+
+import ctypes
+import dataclasses
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+
+INVALID_I16 = -32768
+
+
+@dataclasses.dataclass
+class MatchConfig:
+    """Python mirror of BICOS::Config (reference include/common.hpp:73-82)."""
+    nxcorr_threshold: Optional[float] = 0.5
+    subpixel_step: Optional[float] = None
+    min_variance: Optional[float] = None
+    mode: int = 0              # 0 LIMITED, 1 FULL
+    precision: int = 0         # 0 SINGLE, 1 DOUBLE
+    variant: int = 0           # 0 NoDuplicates, 1 Consistency
+    max_lr_diff: int = 1
+    no_dupes: bool = False
+
+    def to_c(self) -> Tuple[_lib.BicosConfig, int]:
+        thr = self.nxcorr_threshold
+        if thr is not None and not thr >= 0:
+            raise ValueError("device API: nxcorr_threshold must be >= 0 or None "
+                             "(BicosConfig maps negatives to the 0.5 default)")
+        c = _lib.BicosConfig(
+            float(thr if thr is not None else 0.5),
+            float(self.subpixel_step if self.subpixel_step is not None else -1.0),
+            float(self.min_variance if self.min_variance is not None else -1.0),
+            int(self.mode), int(self.precision), int(self.variant), int(self.max_lr_diff),
+            int(bool(self.no_dupes)))
+        return c, int(thr is not None)
+
+
+def _depth(t: torch.Tensor) -> int:
+    if t.dtype == torch.uint8:
+        return 1
+    if t.dtype in (torch.int16, getattr(torch, "uint16", torch.int16)):
+        return 2
+    raise TypeError("stack dtype must be uint8 or (u)int16, got %s" % t.dtype)
+
+
+def _check_stack(t: torch.Tensor):
+    if not t.is_cuda:
+        raise ValueError("device API needs CUDA/HIP tensors")
+    if t.dim() != 3:
+        raise ValueError("stack must be [n, rows, cols]")
+    if t.stride(2) != 1:
+        raise ValueError("stack rows must be contiguous")
+    return t.shape[0], t.shape[1], t.shape[2], t.stride(1), t.stride(0)
+
+
+def _stream(device: torch.device, stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return s.cuda_stream
+
+
+class Engine:
+    """One bicos_engine (workspace + stream-agnostic launcher) per device."""
+
+    def __init__(self, device=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("libbicos_amd device engine needs a ROCm GPU")
+        self.device = torch.device("cuda", torch.cuda.current_device() if device is None
+                                   else torch.device(device).index or 0)
+        self._L = _lib.lib()
+        h = ctypes.c_void_p()
+        _lib.check(self._L.bicos_engine_create(self.device.index, ctypes.byref(h)),
+                   "bicos_engine_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            torch.cuda.synchronize(self.device)
+            self._L.bicos_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ match
+    def match(self, stack0: torch.Tensor, stack1: torch.Tensor,
+              cfg: Optional[MatchConfig] = None, want_corrmap: bool = True,
+              out: Optional[torch.Tensor] = None, corrmap: Optional[torch.Tensor] = None,
+              stream=None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        """Full BICOS::match on device stacks. Returns (disparity, corrmap) on the
+        device; asynchronous on `stream` (default: torch's current stream)."""
+        cfg = cfg or MatchConfig()
+        n, rows, cols, rp, pp = _check_stack(stack0)
+        if tuple(stack1.shape) != (n, rows, cols) or stack1.stride() != stack0.stride() or \
+                stack1.dtype != stack0.dtype:
+            raise ValueError("stack1 must match stack0 in shape, strides and dtype")
+        c, has_nxcorr = cfg.to_c()
+        dev = stack0.device
+        if out is None:
+            out = torch.empty((rows, cols), dtype=torch.float32 if has_nxcorr else torch.int16,
+                              device=dev)
+        if has_nxcorr and want_corrmap and corrmap is None:
+            corrmap = torch.empty((rows, cols), device=dev,
+                                  dtype=torch.float64 if cfg.precision else torch.float32)
+        if not (has_nxcorr and want_corrmap):
+            corrmap = None
+        rc = self._L.bicos_match_device(
+            self._h, stack0.data_ptr(), stack1.data_ptr(), n, rows, cols, rp, pp, _depth(stack0),
+            ctypes.byref(c), has_nxcorr, out.data_ptr(),
+            corrmap.data_ptr() if corrmap is not None else None, _stream(dev, stream))
+        _lib.check(rc, "bicos_match_device")
+        return out, corrmap
+
+    # ----------------------------------------------------------------- stages
+    def transform(self, stack: torch.Tensor, mode: int = 0, words: Optional[int] = None,
+                  out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:
+        """Descriptors as int32 [rows, desc_pitch] (uint32 bit patterns)."""
+        n, rows, cols, rp, pp = _check_stack(stack)
+        words = words or descriptor_words(n, mode)
+        pitch = self._L.bicos_desc_pitch(cols, words)
+        if out is None:
+            out = torch.empty((rows, pitch), dtype=torch.int32, device=stack.device)
+        rc = self._L.bicos_transform_device(stack.data_ptr(), n, rows, cols, rp, pp,
+                                            _depth(stack), mode, words, out.data_ptr(),
+                                            _stream(stack.device, stream))
+        _lib.check(rc, "bicos_transform_device")
+        return out
+
+    def search(self, desc0: torch.Tensor, desc1: torch.Tensor, cols: int, words: int,
+               flags: int = 1, max_lr_diff: int = -1, out: Optional[torch.Tensor] = None,
+               stream=None) -> torch.Tensor:
+        rows = desc0.shape[0]
+        if out is None:
+            out = torch.empty((rows, cols), dtype=torch.int16, device=desc0.device)
+        rc = self._L.bicos_search_device(self._h, desc0.data_ptr(), desc1.data_ptr(), rows, cols,
+                                         words, flags, max_lr_diff, out.data_ptr(),
+                                         _stream(desc0.device, stream))
+        _lib.check(rc, "bicos_search_device")
+        return out
+
+    def agree(self, raw: torch.Tensor, stack0: torch.Tensor, stack1: torch.Tensor,
+              threshold: float, minvar_scaled: Optional[float] = None,
+              step: Optional[float] = None, stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+        n, rows, cols, rp, pp = _check_stack(stack0)
+        out = torch.empty((rows, cols), dtype=torch.float32, device=stack0.device)
+        corr = torch.empty((rows, cols), dtype=torch.float32, device=stack0.device)
+        hm = int(minvar_scaled is not None)
+        mv = float(minvar_scaled or 0.0)
+        st = _stream(stack0.device, stream)
+        if step is None:
+            rc = self._L.bicos_agree_device(raw.data_ptr(), stack0.data_ptr(), stack1.data_ptr(),
+                                            n, rows, cols, rp, pp, _depth(stack0), threshold, hm,
+                                            mv, out.data_ptr(), corr.data_ptr(), st)
+        else:
+            rc = self._L.bicos_subpixel_device(raw.data_ptr(), stack0.data_ptr(),
+                                               stack1.data_ptr(), n, rows, cols, rp, pp,
+                                               _depth(stack0), threshold, step, hm, mv,
+                                               out.data_ptr(), corr.data_ptr(), st)
+        _lib.check(rc, "bicos_agree_device")
+        return out, corr
+
+
+def descriptor_words(n: int, mode: int = 0) -> int:
+    w = _lib.lib().bicos_descriptor_words(n, mode)
+    if w < 0:
+        _lib.check(w, "bicos_descriptor_words")
+    return w
+
+
+_ENGINES = {}
+
+
+def default_engine(device=None) -> Engine:
+    idx = torch.cuda.current_device() if device is None else torch.device(device).index or 0
+    if idx not in _ENGINES:
+        _ENGINES[idx] = Engine(idx)
+    return _ENGINES[idx]
+
+
+def match(stack0: torch.Tensor, stack1: torch.Tensor, cfg: Optional[MatchConfig] = None,
+          **kw) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Module-level convenience: BICOS::match on device tensors."""
+    return default_engine(stack0.device).match(stack0, stack1, cfg, **kw)

@@ -1,0 +1,337 @@
+"""GPU parity: the gfx950 HIP path vs the CPU oracle, through the C-ABI.
+
+Bar (north star): integer disparities bit-exact; nxcorr / subpixel floats within
+1e-4 -- the kernels are written to be bit-exact there too, and these tests
+demand exact equality (the tolerance is only used for Precision::DOUBLE, which
+has no CPU oracle: |corr - float64 numpy| <= 1e-12).
+"""
+import numpy as np
+import pytest
+
+from libbicos_amd.synthetic import random_stack, stereo_stack
+from oracle import ref_numpy as N
+
+pytestmark = pytest.mark.gpu
+
+FLOAT_TOL = 1e-4  # north-star tolerance for nxcorr/subpixel floats (we assert exact below)
+
+
+def dev(a):
+    import torch
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint16:
+        a = a.view(np.int16)
+    return torch.from_numpy(a).cuda()
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def same(a, b):
+    assert a.shape == b.shape, (a.shape, b.shape)
+    assert a.dtype == b.dtype, (a.dtype, b.dtype)
+    if not np.array_equal(a.view(np.uint8), b.view(np.uint8)):
+        if a.dtype.kind == "f":
+            both = np.isnan(a) & np.isnan(b)
+            diff = np.abs(a.astype(np.float64) - b.astype(np.float64))
+            diff[both] = 0
+            bad = np.argwhere(~(diff == 0))
+            raise AssertionError("%d float mismatches, max |d| %g, first %s: %r vs %r" % (
+                len(bad), np.nanmax(diff), bad[0], a[tuple(bad[0])], b[tuple(bad[0])]))
+        bad = np.argwhere(a != b)
+        raise AssertionError("%d mismatches, first %s: %r vs %r" % (
+            len(bad), bad[0], a[tuple(bad[0])], b[tuple(bad[0])]))
+
+
+def cfg_of(O, **kw):
+    return O.OracleConfig(**kw)
+
+
+def gpu_match(eng, L, R, **kw):
+    from libbicos_amd.device import MatchConfig
+    d, c = eng.match(dev(L), dev(R), MatchConfig(**kw))
+    return host(d), (host(c) if c is not None else None)
+
+
+# ----------------------------------------------------------------- transform
+@pytest.mark.parametrize("n,mode,dt", [
+    (2, 0, np.uint8), (3, 0, np.uint8), (4, 0, np.uint8), (8, 0, np.uint8), (9, 0, np.uint16),
+    (10, 0, np.uint8), (17, 0, np.uint8), (33, 0, np.uint8), (33, 0, np.uint16),
+    (40, 0, np.uint8), (45, 0, np.uint8), (65, 0, np.uint16),
+    (2, 1, np.uint8), (3, 1, np.uint8), (4, 1, np.uint8), (8, 1, np.uint16), (10, 1, np.uint8),
+    (16, 1, np.uint8),
+])
+def test_transform_bit_exact(gpu, oracle, n, mode, dt):
+    s = random_stack(n, 13, 301, dt, seed=n * 7 + mode)
+    words = oracle.desc_words(n, mode)
+    ref = oracle.transform(s, mode, words)
+    out = host(gpu.transform(dev(s), mode, words)).view(np.uint32)
+    same(out[:, : 301 * words].reshape(13, 301, words), ref)
+
+
+# -------------------------------------------------------------------- search
+def _low_entropy_desc(H, W, words, seed, bits=6):
+    rng = np.random.default_rng(seed)
+    d = rng.integers(0, 2 ** 32, size=(H, W, words), dtype=np.uint64).astype(np.uint32)
+    mask = np.uint32((1 << bits) - 1)
+    d[..., 1:] = 0
+    d[..., 0] &= mask     # forces many exact duplicate minima
+    return d
+
+
+def _pack(desc):
+    H, W, words = desc.shape
+    from libbicos_amd import _lib
+    pitch = _lib.lib().bicos_desc_pitch(W, words)
+    out = np.zeros((H, pitch), np.uint32)
+    out[:, : W * words] = desc.reshape(H, W * words)
+    return out.view(np.int32)
+
+
+@pytest.mark.parametrize("words", [1, 2, 4, 8])
+@pytest.mark.parametrize("flags,lr", [(1, -1), (2, 1), (3, 1), (2, 0), (3, 5)])
+@pytest.mark.parametrize("W", [1, 7, 64, 333, 1030])
+def test_search_bit_exact(gpu, oracle, words, flags, lr, W):
+    H = 5
+    rng = np.random.default_rng(words * 1000 + W)
+    d0 = rng.integers(0, 2 ** 32, size=(H, W, words), dtype=np.uint64).astype(np.uint32)
+    d1 = d0[:, np.roll(np.arange(W), 3)] ^ (rng.random((H, W, words)) < 0.02).astype(np.uint32)
+    for a, b in ((d0, d1), (_low_entropy_desc(H, W, words, 1), _low_entropy_desc(H, W, words, 2))):
+        ref = oracle.search(a, b, flags, lr)
+        out = host(gpu.search(dev(_pack(a)), dev(_pack(b)), W, words, flags, lr))
+        same(out, ref)
+
+
+def test_search_multi_chunk(gpu, oracle):
+    # W * 32 B > 64 KiB LDS stage -> the right row is streamed in chunks
+    H, W, words = 2, 3001, 8
+    rng = np.random.default_rng(9)
+    a = rng.integers(0, 2 ** 32, size=(H, W, words), dtype=np.uint64).astype(np.uint32)
+    b = a[:, ::-1].copy()
+    b[..., 0] ^= 1
+    for flags, lr in ((1, -1), (3, 2)):
+        same(host(gpu.search(dev(_pack(a)), dev(_pack(b)), W, words, flags, lr)),
+             oracle.search(a, b, flags, lr))
+
+
+# --------------------------------------------------------------------- agree
+@pytest.mark.parametrize("n,dt", [(2, np.uint8), (8, np.uint8), (33, np.uint8), (17, np.uint16),
+                                  (40, np.uint8), (65, np.uint8)])
+@pytest.mark.parametrize("minvar", [None, 2.0])
+def test_agree_bit_exact(gpu, oracle, n, dt, minvar):
+    H, W = 9, 200
+    L, R = stereo_stack(n, H, W, dt, dmin=3, drange=20, seed=n)
+    rng = np.random.default_rng(n)
+    raw = rng.integers(-5, 30, size=(H, W)).astype(np.int16)
+    raw[rng.random((H, W)) < 0.2] = -32768
+    R[:, 0, 40] = 9  # constant right pixel -> NaN correlation
+    raw[0, 45] = 5
+    mv = None if minvar is None else np.float32(minvar) * np.float32(n)
+    rd, rc = oracle.agree(raw, L, R, 0.5, mv)
+    out, corr = gpu.agree(dev(raw), dev(L), dev(R), 0.5, None if mv is None else float(mv))
+    same(host(out), rd.astype(np.float32))
+    same(host(corr), rc)
+
+
+@pytest.mark.parametrize("n,dt", [(2, np.uint8), (8, np.uint8), (12, np.uint16), (33, np.uint8),
+                                  (33, np.uint16), (40, np.uint8), (65, np.uint8)])
+@pytest.mark.parametrize("step,minvar", [(0.1, None), (0.25, 1.0), (0.05, None)])
+def test_subpixel_bit_exact(gpu, oracle, n, dt, step, minvar):
+    H, W = 7, 160
+    L = random_stack(n, H, W, dt, seed=n + 1)
+    R = random_stack(n, H, W, dt, seed=n + 2)
+    rng = np.random.default_rng(n)
+    raw = rng.integers(-3, 12, size=(H, W)).astype(np.int16)
+    raw[:, 3] = 3            # col1 == 0 edge
+    raw[:, W - 1] = 0        # col1 == W-1 edge
+    raw[rng.random((H, W)) < 0.1] = -32768
+    mv = None if minvar is None else np.float32(minvar) * np.float32(n)
+    ro, rc = oracle.agree_subpixel(raw, L, R, 0.2, step, mv)
+    out, corr = gpu.agree(dev(raw), dev(L), dev(R), 0.2, None if mv is None else float(mv),
+                          step=step)
+    same(host(out), ro)
+    same(host(corr), rc)
+
+
+# -------------------------------------------------------------- full match
+CFGS = [
+    dict(nxcorr_threshold=None),
+    dict(nxcorr_threshold=0.9),
+    dict(nxcorr_threshold=0.96, min_variance=2.0),
+    dict(nxcorr_threshold=0.96, min_variance=2.0, subpixel_step=0.1),
+    dict(nxcorr_threshold=0.5, variant=1, max_lr_diff=1),
+    dict(nxcorr_threshold=None, variant=1, max_lr_diff=3, no_dupes=True),
+]
+
+
+@pytest.mark.parametrize("n,H,W,dt,mode", [
+    (8, 24, 640, np.uint8, 0), (33, 16, 2048, np.uint8, 0), (40, 8, 1024, np.uint8, 0),
+    (17, 12, 700, np.uint16, 0), (10, 12, 300, np.uint8, 1), (16, 6, 257, np.uint16, 1),
+    (2, 5, 96, np.uint8, 0), (65, 4, 400, np.uint8, 0),
+])
+def test_match_bit_exact(gpu, oracle, n, H, W, dt, mode):
+    L, R = stereo_stack(n, H, W, dt)
+    for cfg in CFGS:
+        ref = oracle.match(L, R, cfg_of(oracle, mode=mode, **cfg))
+        got = gpu_match(gpu, L, R, mode=mode, **cfg)
+        same(got[0], ref[0])
+        if ref[1] is not None:
+            same(got[1], ref[1])
+
+
+def test_cfg1_through_pybicos(gpu, oracle):
+    """BASELINE configs[0]: 8-image 640x480 stack, nxcorr 0.9, via pybicos.match."""
+    import pybicos
+    L, R = stereo_stack(8, 480, 640)
+    cfg = pybicos.Config()
+    cfg.nxcorr_threshold = 0.9
+    d, c = pybicos.match(list(L), list(R), cfg)
+    rd, rc = oracle.match(L, R, oracle.OracleConfig(nxcorr_threshold=0.9))
+    assert d.dtype == np.float32 and c.dtype == np.float32
+    same(d, rd)
+    same(c, rc)
+
+
+def test_pybicos_consistency_and_subpixel(gpu, oracle):
+    import pybicos
+    L, R = stereo_stack(40, 12, 512, np.uint16)
+    cfg = pybicos.Config()
+    cfg.nxcorr_threshold = 0.6
+    cfg.subpixel_step = 0.25
+    cfg.min_variance = 1.0
+    cfg.set_consistency(max_lr_diff=2, no_dupes=True)
+    d, c = pybicos.match(list(L), list(R), cfg)
+    rd, rc = oracle.match(L, R, oracle.OracleConfig(nxcorr_threshold=0.6, subpixel_step=0.25,
+                                                    min_variance=1.0, variant=1, max_lr_diff=2,
+                                                    no_dupes=True))
+    same(d, rd)
+    same(c, rc)
+
+
+# ------------------------------------------------- full size (BASELINE shapes)
+def _full_size_check(gpu, oracle, n, H, W, cfg, rows):
+    L, R = stereo_stack(n, H, W)
+    got_d, got_c = gpu_match(gpu, L, R, **cfg)
+    # rows are independent: the oracle on a band of rows equals those rows of the frame
+    for (b, e) in rows:
+        rd, rc = oracle.match(L[:, b:e], R[:, b:e], oracle.OracleConfig(**cfg))
+        same(got_d[b:e].copy(), rd)
+        if rc is not None:
+            same(got_c[b:e].copy(), rc)
+    truth = (16 + (48 * np.arange(H)) // H)[:, None]
+    d = got_d.astype(np.float64)
+    valid = np.isfinite(d) & (d != -32768)
+    return valid, np.abs(d - truth)
+
+
+def test_cfg2_full_size(gpu, oracle):
+    """2048x1536x33 LIMITED (128-bit), thr 0.96: oracle-checked bands + planted truth."""
+    valid, err = _full_size_check(gpu, oracle, 33, 1536, 2048, dict(nxcorr_threshold=0.96),
+                                  [(0, 8), (760, 768), (1528, 1536)])
+    assert valid.mean() > 0.95
+    assert (err[valid] == 0).mean() > 0.99
+
+
+def test_cfg3_full_size(gpu, oracle):
+    valid, err = _full_size_check(gpu, oracle, 33, 1536, 2048,
+                                  dict(nxcorr_threshold=0.96, min_variance=2.0, subpixel_step=0.1),
+                                  [(100, 104), (1200, 1204)])
+    assert valid.mean() > 0.9
+    assert (err[valid] <= 1.0).all()
+
+
+def test_cfg4_full_size(gpu, oracle):
+    valid, err = _full_size_check(gpu, oracle, 40, 1536, 2048,
+                                  dict(nxcorr_threshold=0.96, variant=1, max_lr_diff=1),
+                                  [(0, 4), (1000, 1004)])
+    assert valid.mean() > 0.9
+
+
+def test_row_band_sharding_is_exact(gpu):
+    """Sharded bands (as the multi-GPU path computes them) == the whole-frame match."""
+    L, R = stereo_stack(33, 96, 1024)
+    cfg = dict(nxcorr_threshold=0.96, min_variance=2.0, subpixel_step=0.1)
+    full_d, full_c = gpu_match(gpu, L, R, **cfg)
+    from libbicos_amd.distributed import band_rows
+    for world in (2, 3, 8):
+        parts = [gpu_match(gpu, L[:, b:e], R[:, b:e], **cfg)
+                 for b, e in (band_rows(96, world, r) for r in range(world))]
+        same(np.concatenate([p[0] for p in parts]), full_d)
+        same(np.concatenate([p[1] for p in parts]), full_c)
+
+
+# ---------------------------------------------------------------- edge cases
+def test_empty_and_tiny(gpu, oracle):
+    from libbicos_amd.device import MatchConfig
+    import torch
+    z = torch.zeros((4, 0, 10), dtype=torch.uint8, device="cuda")
+    d, c = gpu.match(z, z, MatchConfig())
+    assert d.shape == (0, 10)
+    z = torch.zeros((4, 3, 0), dtype=torch.uint8, device="cuda")
+    d, c = gpu.match(z, z, MatchConfig())
+    assert d.shape == (3, 0)
+    L, R = stereo_stack(8, 1, 1)
+    for cfg in CFGS:
+        same(gpu_match(gpu, L, R, **cfg)[0], oracle.match(L, R, cfg_of(oracle, **cfg))[0])
+
+
+def test_errors(gpu):
+    import torch
+    from libbicos_amd import BicosError
+    from libbicos_amd.device import MatchConfig
+    s = torch.zeros((1, 4, 4), dtype=torch.uint8, device="cuda")
+    with pytest.raises(BicosError, match="at least two"):
+        gpu.match(s, s)
+    s = torch.zeros((66, 4, 4), dtype=torch.uint8, device="cuda")
+    with pytest.raises(BicosError, match="too large"):
+        gpu.match(s, s)
+    s = torch.zeros((17, 4, 4), dtype=torch.uint8, device="cuda")
+    with pytest.raises(BicosError, match="too large"):
+        gpu.match(s, s, MatchConfig(mode=1))
+    s = torch.zeros((8, 4, 4), dtype=torch.uint8, device="cuda")
+    with pytest.raises(BicosError, match="subpixel_step"):
+        gpu.match(s, s, MatchConfig(subpixel_step=0.0))
+
+
+def test_pybicos_errors(gpu):
+    import pybicos
+    a = [np.zeros((8, 8), np.uint8)] * 8
+    b = [np.zeros((8, 9), np.uint8)] * 8
+    with pytest.raises(RuntimeError):
+        pybicos.match(a, b)
+    with pytest.raises(RuntimeError):
+        pybicos.match(a[:1], a[:1])
+    with pytest.raises(ValueError):
+        pybicos.match([np.zeros((8, 8), np.int32)] * 8, a)
+
+
+def test_double_precision(gpu, oracle):
+    """Precision::DOUBLE (CUDA-build feature, agree.cuh:35-65): no CPU oracle; compare
+    the float64 correlation with a float64 numpy restatement (no fma there: 1e-12)."""
+    L, R = stereo_stack(33, 8, 512)
+    d32, c32 = gpu_match(gpu, L, R, nxcorr_threshold=0.5)
+    d64, c64 = gpu_match(gpu, L, R, nxcorr_threshold=0.5, precision=1)
+    assert c64.dtype == np.float64
+    raw, _ = oracle.match(L, R, oracle.OracleConfig(nxcorr_threshold=None))
+    rr, cc = np.nonzero(raw != -32768)
+    col1 = cc - raw[rr, cc].astype(np.int64)
+    ok = (col1 >= 0) & (col1 < 512)
+    rr, cc, col1 = rr[ok], cc[ok], col1[ok]
+    a = L[:, rr, cc].astype(np.float64)
+    b = R[:, rr, col1].astype(np.float64)
+    a -= a.mean(0)
+    b -= b.mean(0)
+    ref = (a * b).sum(0) / np.sqrt((a * a).sum(0) * (b * b).sum(0))
+    got = c64[rr, cc]
+    fin = np.isfinite(ref)
+    assert np.abs(got[fin] - ref[fin]).max() < 1e-12
+    assert np.abs(c32[rr, cc][fin] - ref[fin]).max() < FLOAT_TOL
+
+
+def test_deterministic(gpu):
+    L, R = stereo_stack(33, 32, 1024)
+    a = gpu_match(gpu, L, R, nxcorr_threshold=0.9, subpixel_step=0.1)
+    b = gpu_match(gpu, L, R, nxcorr_threshold=0.9, subpixel_step=0.1)
+    same(a[0], b[0])
+    same(a[1], b[1])

@@ -1,0 +1,80 @@
+// valu_peak.hip -- measures the sustained wave64 issue rate of the integer VALU ops the
+// BICOS search loop is made of (v_xor_b32, v_bcnt_u32_b32, v_min_u32, v_med3_u32,
+// v_lshl_or_b32) on the running MI355X, to price the search kernel's roofline
+// against a measured, not assumed, peak. Independent chains, 8 waves/SIMD.
+//   hipcc --offload-arch=gfx950 -O3 tools/valu_peak.hip -o build/valu_peak && build/valu_peak
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdint>
+
+#define CHAINS 8
+#define ITERS 4096
+
+template <int OP>
+__global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
+    uint32_t v[CHAINS], w[CHAINS];
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) {
+        v[c] = seed * (threadIdx.x + 1) + c;
+        w[c] = seed ^ (c * 0x9E3779B9u) ^ blockIdx.x;
+    }
+    for (int i = 0; i < ITERS; ++i) {
+#pragma unroll
+        for (int c = 0; c < CHAINS; ++c) {
+            if (OP == 0) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 1) asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 2) asm volatile("v_min_u32 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 3) asm volatile("v_med3_u32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
+            if (OP == 4) asm volatile("v_lshl_or_b32 %0, %0, 16, %1" : "+v"(v[c]) : "v"(w[c]));
+        }
+    }
+    uint32_t r = 0;
+#pragma unroll
+    for (int c = 0; c < CHAINS; ++c) r ^= v[c];
+    if (r == 0x12345678u) out[blockIdx.x] = r;
+}
+
+template <int OP>
+double run(const char* name, uint32_t* out, int grid) {
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL(k<OP>, dim3(grid), dim3(256), 0, 0, out, 3u);
+    hipDeviceSynchronize();
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; ++rep) {
+        hipEventRecord(a);
+        hipLaunchKernelGGL(k<OP>, dim3(grid), dim3(256), 0, 0, out, 3u + rep);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        if (ms < best) best = ms;
+    }
+    const double ops = (double)grid * 256 * ITERS * CHAINS;  // lane-ops
+    const double tops = ops / (best * 1e-3) / 1e12;
+    printf("{\"op\": \"%s\", \"lane_ops\": %.3e, \"ms\": %.4f, \"Tops\": %.2f}\n", name, ops, best, tops);
+    return tops;
+}
+
+int main() {
+    hipDeviceProp_t p;
+    hipGetDeviceProperties(&p, 0);
+    int clk = 0;
+    hipDeviceGetAttribute(&clk, hipDeviceAttributeClockRate, 0);
+    printf("{\"device\": \"%s\", \"gcnArch\": \"%s\", \"CUs\": %d, \"clock_khz\": %d, "
+           "\"nominal_int32_Tops\": %.2f}\n",
+           p.name, p.gcnArchName, p.multiProcessorCount, clk,
+           p.multiProcessorCount * 128.0 * clk * 1e3 / 1e12);
+    uint32_t* out;
+    hipMalloc(&out, 1 << 20);
+    const int grid = p.multiProcessorCount * 8 * 4;  // 8 waves/SIMD worth of 256-thr blocks x4
+    run<0>("v_xor_b32", out, grid);
+    run<1>("v_bcnt_u32_b32", out, grid);
+    run<2>("v_min_u32", out, grid);
+    run<3>("v_med3_u32", out, grid);
+    run<4>("v_lshl_or_b32", out, grid);
+    hipFree(out);
+    return 0;
+}
