@@ -99,6 +99,15 @@ typedef struct bicos_engine bicos_engine;
 int bicos_engine_create(int device, bicos_engine** out);
 void bicos_engine_destroy(bicos_engine* e);
 
+/* Search-kernel tuning for this engine (0 = automatic for each argument):
+ *   variant        16 = packed 16-bit keys (default), 17 = the same with the inner step
+ *                  as one inline-asm block, 32 = 32-bit keys
+ *   col0_per_lane  left pixels held in registers per lane (16: 2|4; 32: 1|2|4)
+ *   waves          waves per workgroup (1..8)
+ *   split          waves that share one col0 group and split its col1 scan (1|2|4, variant 16)
+ * Results are identical for every setting; only speed changes. */
+int bicos_engine_tune(bicos_engine* e, int variant, int col0_per_lane, int waves, int split);
+
 /* Descriptor width in 32-bit words for n images in `mode` (reference dispatch
  * src/impl/cpu.cpp:122-156); BICOS_E_BITS when more than 256 bits are needed. */
 int bicos_descriptor_words(int n, int mode);

@@ -55,7 +55,7 @@ class BicosResult(ctypes.Structure):
 EXPORTS = (
     "BICOS_CreateDefaultConfig", "BICOS_FreeConfig", "BICOS_FreeResult", "BICOS_Match",
     "BICOS_InvalidDisparityFloat", "BICOS_InvalidDisparityInt16", "bicos_last_error",
-    "bicos_engine_create", "bicos_engine_destroy", "bicos_descriptor_words", "bicos_output_type",
+    "bicos_engine_create", "bicos_engine_destroy", "bicos_engine_tune", "bicos_descriptor_words", "bicos_output_type",
     "bicos_match_device", "bicos_desc_pitch", "bicos_transform_device", "bicos_search_device",
     "bicos_agree_device", "bicos_subpixel_device", "bicos_build_info",
 )
@@ -108,6 +108,8 @@ def lib() -> ctypes.CDLL:
     L.bicos_engine_create.restype = I
     L.bicos_engine_destroy.argtypes = [P]
     L.bicos_engine_destroy.restype = None
+    L.bicos_engine_tune.argtypes = [P, I, I, I, I]
+    L.bicos_engine_tune.restype = I
     L.bicos_descriptor_words.argtypes = [I, I]
     L.bicos_descriptor_words.restype = I
     L.bicos_output_type.argtypes = [ctypes.POINTER(BicosConfig), I]

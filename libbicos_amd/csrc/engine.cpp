@@ -75,6 +75,13 @@ int descriptor_words(int n, int mode) {
     return BICOS_E_BITS;
 }
 
+bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, int words) {
+    const int max_lds = e ? e->max_lds : 64 * 1024;
+    if (!e) return bicos_hip::search_geometry(rows, cols, words, max_lds);
+    return bicos_hip::search_geometry(rows, cols, words, max_lds, e->tune_variant, e->tune_R,
+                                      e->tune_waves, e->tune_split);
+}
+
 static int required_bits(int n, int mode) { return mode ? n * n - 2 * n + 3 : 4 * n - 7; }
 
 int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int rows, int cols,
@@ -129,7 +136,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     if (rc) return rc;
 
     // 2. bicos search (cpu.cpp:68-75)
-    const bicos_hip::SearchGeometry g = bicos_hip::search_geometry(rows, cols, words, e->max_lds);
+    const bicos_hip::SearchGeometry g = geometry(e, rows, cols, words);
     if (!consistency) {
         bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
         rc = check_hip(bicos_hip::launch_search(sa, g, words, true, st), "search launch");
@@ -236,6 +243,26 @@ void bicos_engine_destroy(bicos_engine* e) {
     delete e;
 }
 
+int bicos_engine_tune(bicos_engine* e, int variant, int col0_per_lane, int waves, int split) {
+    if (!e) return fail(BICOS_E_ARG, "null engine");
+    if (variant != 0 && variant != 16 && variant != 17 && variant != 32)
+        return fail(BICOS_E_ARG, "variant 0|16|17|32");
+    const int v = variant == 17 ? 16 : (variant ? variant : 16);
+    if (col0_per_lane != 0 && !(v == 16 ? (col0_per_lane == 2 || col0_per_lane == 4)
+                                        : (col0_per_lane == 1 || col0_per_lane == 2 ||
+                                           col0_per_lane == 4)))
+        return fail(BICOS_E_ARG, "col0_per_lane: 2|4 (variant 16), 1|2|4 (variant 32)");
+    if (waves < 0 || waves > 8) return fail(BICOS_E_ARG, "waves 1..8");
+    if (split != 0 && split != 1 && split != 2 && split != 4) return fail(BICOS_E_ARG, "split 1|2|4");
+    if (split > 1 && (v != 16 || (waves ? waves : 8) % split))
+        return fail(BICOS_E_ARG, "split needs variant 16 and waves divisible by split");
+    e->tune_variant = variant;
+    e->tune_R = col0_per_lane;
+    e->tune_waves = waves;
+    e->tune_split = split;
+    return BICOS_OK;
+}
+
 int bicos_descriptor_words(int n, int mode) {
     if (n < 2) return fail(BICOS_E_ARG, "need at least two images");
     const int w = descriptor_words(n, mode ? 1 : 0);
@@ -294,8 +321,7 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     hipStream_t st = (hipStream_t)stream;
     const size_t dpitch = bicos_desc_pitch(cols, words);
     const bool nodupes = (flags & 1) != 0;
-    const int max_lds = e ? e->max_lds : 64 * 1024;
-    const bicos_hip::SearchGeometry g = bicos_hip::search_geometry(rows, cols, words, max_lds);
+    const bicos_hip::SearchGeometry g = geometry(e, rows, cols, words);
     if (!(flags & 2)) {
         bicos_hip::SearchArgs sa{desc0, desc1, out, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
         return check_hip(bicos_hip::launch_search(sa, g, words, nodupes, st), "search launch");

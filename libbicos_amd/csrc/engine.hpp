@@ -16,6 +16,8 @@
 struct bicos_engine {
     int device = 0;
     int max_lds = 64 * 1024;
+    // search kernel tuning (0 = automatic): see bicos_engine_tune
+    int tune_variant = 0, tune_R = 0, tune_waves = 0, tune_split = 0;
     hipStream_t own_stream = nullptr;  // used by the host-buffer APIs
     std::mutex lock;                   // serialises host-buffer calls on this engine
 
@@ -43,6 +45,8 @@ int check_hip(hipError_t e, const char* what);
 int reserve(void*& buf, size_t& have, size_t bytes, int device);
 
 int descriptor_words(int n, int mode);
+
+bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, int words);
 
 // Full match on device buffers (validated arguments). corr may be null.
 int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int rows, int cols,

@@ -167,6 +167,79 @@ __global__ __launch_bounds__(256) void transform_kernel(TransformArgs a) {
     }
 }
 
+// LIMITED transform with the n samples of a pixel held in registers (MAXN >= n bounds
+// the static arrays; t >= n slots are skipped by wave-uniform branches) and every loop
+// bit at a compile-time position: t = 0, 1 emit bits 3t..3t+2, t >= 2 emits bits
+// 6+4(t-2) .. 9+4(t-2) (a<b, a<c, a<av, ps[t-2]<ps[t]); only the 4 tail bits land at an
+// n-dependent position. One load per sample (the two-pass kernel above re-reads them).
+template <typename TIn, int WORDS, int MAXN>
+__global__ __launch_bounds__(256) void transform_limited_kernel(TransformArgs a) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    const int row = blockIdx.y;
+    const int which = blockIdx.z;
+    if (col >= a.cols) return;
+    const TIn* __restrict__ p = (const TIn*)(which ? a.stack1 : a.stack0) + (size_t)row * a.row_pitch + col;
+    uint32_t* __restrict__ out = (which ? a.desc1 : a.desc0) + (size_t)row * a.desc_pitch + (size_t)col * WORDS;
+    const size_t pp = a.plane_pitch;
+    const int n = a.n;
+
+    uint32_t v[MAXN];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int t = 0; t < MAXN; ++t)
+        if (t < n) {
+            v[t] = ld(p + t * pp);
+            sum += v[t];
+        }
+    // exact: integer sum == the reference's sequential float sum (< 2^24)
+    const float av = fdiv_rn((float)sum, (float)n);
+
+    uint32_t w[WORDS];
+#pragma unroll
+    for (int k = 0; k < WORDS; ++k) w[k] = 0;
+#define BICOS_SET(pos, cond) w[(pos) >> 5] |= (uint32_t)(cond) << ((pos) & 31)
+#pragma unroll
+    for (int t = 0; t < MAXN - 2; ++t) {
+        if (t < n - 2) {
+            const uint32_t x = v[t], y = v[t + 1], z = v[t + 2];
+            const int pos = t < 2 ? 3 * t : 6 + 4 * (t - 2);
+            BICOS_SET(pos + 0, x < y);
+            BICOS_SET(pos + 1, x < z);
+            BICOS_SET(pos + 2, (float)x < av);
+            if (t >= 2) BICOS_SET(pos + 3, v[t - 2] + v[t - 1] < x + y);
+        }
+    }
+#undef BICOS_SET
+    // tail (descriptor_transform.hpp:63-68): a = p[n-2], b = p[n-1]
+    uint32_t x = 0, y = 0, pm2 = 0;
+#pragma unroll
+    for (int t = 0; t < MAXN; ++t) {
+        if (t == n - 2) x = v[t];
+        if (t == n - 1) y = v[t];
+        if (t == n - 4) pm2 = v[t] + v[t + 1];
+    }
+    const uint32_t tail = (uint32_t)(x < y) | ((uint32_t)((float)x < av) << 1) |
+                          ((uint32_t)((float)y < av) << 2) |
+                          ((uint32_t)(n < 4 || pm2 < x + y) << 3);
+    const int tpos = n >= 4 ? 3 * (n - 2) + (n - 4) : 3 * (n - 2);
+    const int tw = tpos >> 5, toff = tpos & 31;
+#pragma unroll
+    for (int k = 0; k < WORDS; ++k) {
+        if (k == tw) w[k] |= tail << toff;
+        if (k == tw + 1 && toff > 28) w[k] |= tail >> (32 - toff);
+    }
+
+    if (WORDS % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < WORDS; k += 4)
+            *(uint4*)(out + k) = make_uint4(w[k], w[k + 1], w[k + 2], w[k + 3]);
+    } else if (WORDS == 2) {
+        *(uint2*)out = make_uint2(w[0], w[1 % WORDS]);
+    } else {
+        out[0] = w[0];
+    }
+}
+
 // --------------------------------------------------------------------- search
 
 // Hamming cost of one (col0, col1) pair.
@@ -302,6 +375,276 @@ __global__ __launch_bounds__(512) void search_kernel(SearchArgs a) {
     }
 }
 
+// ---- packed 16-bit key variant ---------------------------------------------------
+//
+// Measured on MI355X (tools/valu_peak.hip): v_xor/v_and/v_add issue at full rate
+// (~72 T lane-op/s) but v_bcnt, v_min, v_med3, v_lshl_or, v_perm and v_pk_*_u16 at half
+// rate (~38.5 T). The 32-bit-key loop above spends 7 half-rate ops per pair (w bcnt +
+// lshl_or + med3 + min for w = 4). Here two col0 share one 32-bit register of two 16-bit
+// keys (cost << 8 | col1 within a 256-column tile):
+//   r0, r1  = bcnt chains seeded with (col1_local << 8)  -> byte1 = col1, byte0 = cost
+//   key     = v_perm_b32(r1, r0)      [r0.b1 r0.b0 | r1.b1 r1.b0]  (1 op / 2 pairs)
+//   lo      = v_pk_min_u16(lo, key)   first minimum (lowest col1)  (1 op / 2 pairs)
+//   hi      = v_pk_min_u16(hi, key ^ 0x00FF00FF)   last minimum    (1 op + 1 fast xor)
+// The minimum is duplicated iff its first and last columns differ. Tiles fold into
+// 32-bit keys (cost << 16 | col1). Costs must fit 8 bits: descriptors from the transform
+// use <= 254 bits (LIMITED 4n-6 <= 254, FULL n^2-2n+3 <= 227), and bit 255 is masked
+// on both sides when the descriptor has 256 bits, so cost <= 255.
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+
+// One col1 step for one packed pair (col0 a -> low half, col0 b -> high half) as ONE asm
+// block: hipcc pads every use of a value defined by an asm statement with an s_nop, and
+// lets the compiler re-associate the bcnt chain into v_add3 trees otherwise; measured
+// (tools/search_variants.hip): full-asm step 1.6-8 % faster than the asm-opaque chain,
+// 25 % faster than plain C. Emitted per word k: two v_xor (full rate) + two v_bcnt chained
+// through r0/r1 (seeded with col1_local << 8 by the first bcnt); then one v_perm_b32 and
+// v_pk_min_u16 for the first minimum, one v_xor + v_pk_min_u16 for the last minimum.
+#define BICOS_XB(k, first)                                      \
+    "v_xor_b32 %[t0], %[d" #k "], %[a" #k "]\n\t"                \
+    "v_xor_b32 %[t1], %[d" #k "], %[b" #k "]\n\t"                \
+    "v_bcnt_u32_b32 %[r0], %[t0], " first "\n\t"                \
+    "v_bcnt_u32_b32 %[r1], %[t1], " first "\n\t"
+#define BICOS_XB_NEXT(k)                                        \
+    "v_xor_b32 %[t0], %[d" #k "], %[a" #k "]\n\t"                \
+    "v_xor_b32 %[t1], %[d" #k "], %[b" #k "]\n\t"                \
+    "v_bcnt_u32_b32 %[r0], %[t0], %[r0]\n\t"                    \
+    "v_bcnt_u32_b32 %[r1], %[t1], %[r1]\n\t"
+#define BICOS_PACK_MIN                                          \
+    "v_perm_b32 %[r0], %[r1], %[r0], %[sel]\n\t"                \
+    "v_pk_min_u16 %[lo], %[lo], %[r0]\n\t"
+#define BICOS_PACK_MAX_TOO                                      \
+    "v_xor_b32 %[r0], 0xff00ff, %[r0]\n\t"                      \
+    "v_pk_min_u16 %[hi], %[hi], %[r0]\n\t"
+#define BICOS_OPS4(o)                                                                    \
+    [d0] "v"(d1[o + 0]), [d1] "v"(d1[o + 1]), [d2] "v"(d1[o + 2]), [d3] "v"(d1[o + 3]),  \
+        [a0] "v"(a[o + 0]), [a1] "v"(a[o + 1]), [a2] "v"(a[o + 2]), [a3] "v"(a[o + 3]),  \
+        [b0] "v"(b[o + 0]), [b1] "v"(b[o + 1]), [b2] "v"(b[o + 2]), [b3] "v"(b[o + 3])
+
+template <int WORDS, bool HI>
+__device__ __forceinline__ void pair_step(const uint32_t (&d1)[WORDS], const uint32_t (&a)[WORDS],
+                                          const uint32_t (&b)[WORDS], uint32_t seed, uint32_t& lo,
+                                          uint32_t& hi) {
+    uint32_t t0, t1, r0, r1;
+    const uint32_t sel = 0x04050001u;  // key = [r0.b1 r0.b0 | r1.b1 r1.b0]
+    if constexpr (WORDS == 1) {
+        if (HI)
+            asm(BICOS_XB(0, "%[seed]") BICOS_PACK_MIN BICOS_PACK_MAX_TOO
+                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1), [lo] "+v"(lo), [hi] "+v"(hi)
+                : [d0] "v"(d1[0]), [a0] "v"(a[0]), [b0] "v"(b[0]), [seed] "s"(seed), [sel] "s"(sel));
+        else
+            asm(BICOS_XB(0, "%[seed]") BICOS_PACK_MIN
+                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1), [lo] "+v"(lo)
+                : [d0] "v"(d1[0]), [a0] "v"(a[0]), [b0] "v"(b[0]), [seed] "s"(seed), [sel] "s"(sel));
+    } else if constexpr (WORDS == 2) {
+        if (HI)
+            asm(BICOS_XB(0, "%[seed]") BICOS_XB_NEXT(1) BICOS_PACK_MIN BICOS_PACK_MAX_TOO
+                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1), [lo] "+v"(lo), [hi] "+v"(hi)
+                : [d0] "v"(d1[0]), [d1] "v"(d1[1]), [a0] "v"(a[0]), [a1] "v"(a[1]), [b0] "v"(b[0]),
+                  [b1] "v"(b[1]), [seed] "s"(seed), [sel] "s"(sel));
+        else
+            asm(BICOS_XB(0, "%[seed]") BICOS_XB_NEXT(1) BICOS_PACK_MIN
+                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1), [lo] "+v"(lo)
+                : [d0] "v"(d1[0]), [d1] "v"(d1[1]), [a0] "v"(a[0]), [a1] "v"(a[1]), [b0] "v"(b[0]),
+                  [b1] "v"(b[1]), [seed] "s"(seed), [sel] "s"(sel));
+    } else if constexpr (WORDS == 4) {
+        if (HI)
+            asm(BICOS_XB(0, "%[seed]") BICOS_XB_NEXT(1) BICOS_XB_NEXT(2) BICOS_XB_NEXT(3)
+                    BICOS_PACK_MIN BICOS_PACK_MAX_TOO
+                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1), [lo] "+v"(lo), [hi] "+v"(hi)
+                : BICOS_OPS4(0), [seed] "s"(seed), [sel] "s"(sel));
+        else
+            asm(BICOS_XB(0, "%[seed]") BICOS_XB_NEXT(1) BICOS_XB_NEXT(2) BICOS_XB_NEXT(3)
+                    BICOS_PACK_MIN
+                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1), [lo] "+v"(lo)
+                : BICOS_OPS4(0), [seed] "s"(seed), [sel] "s"(sel));
+    } else {
+        // 8 words: two blocks (inline asm takes at most 30 operands)
+        asm(BICOS_XB(0, "%[seed]") BICOS_XB_NEXT(1) BICOS_XB_NEXT(2) BICOS_XB_NEXT(3)
+            : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1)
+            : BICOS_OPS4(0), [seed] "s"(seed));
+        if (HI)
+            asm(BICOS_XB_NEXT(0) BICOS_XB_NEXT(1) BICOS_XB_NEXT(2) BICOS_XB_NEXT(3)
+                    BICOS_PACK_MIN BICOS_PACK_MAX_TOO
+                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "+&v"(r0), [r1] "+&v"(r1), [lo] "+v"(lo), [hi] "+v"(hi)
+                : BICOS_OPS4(4), [sel] "s"(sel));
+        else
+            asm(BICOS_XB_NEXT(0) BICOS_XB_NEXT(1) BICOS_XB_NEXT(2) BICOS_XB_NEXT(3) BICOS_PACK_MIN
+                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "+&v"(r0), [r1] "+&v"(r1), [lo] "+v"(lo)
+                : BICOS_OPS4(4), [sel] "s"(sel));
+    }
+}
+
+// The same step in C with an instruction-free asm keeping each bcnt accumulator opaque
+// (so the chain is not re-associated into v_add3); the compiler schedules freely.
+template <int WORDS>
+__device__ __forceinline__ uint32_t ham_seeded(const uint32_t (&a)[WORDS], const uint32_t (&b)[WORDS],
+                                               uint32_t seed) {
+    uint32_t c = bcnt_acc(a[0] ^ b[0], seed);
+#pragma unroll
+    for (int k = 1; k < WORDS; ++k) c = bcnt_acc(a[k] ^ b[k], c);
+    return c;
+}
+
+template <int WORDS, bool NODUPES, int RP, int STEP>
+__device__ __forceinline__ void search16_step(const uint32_t* s, uint32_t seed,
+                                              const uint32_t (&d0)[2 * RP][WORDS],
+                                              uint32_t (&lo)[RP], uint32_t (&hi)[RP]) {
+    uint32_t d1[WORDS];
+    lds_fetch<WORDS>(s, d1);
+#pragma unroll
+    for (int p = 0; p < RP; ++p) {
+        if (STEP == 1) {
+            pair_step<WORDS, NODUPES>(d1, d0[2 * p], d0[2 * p + 1], seed, lo[p], hi[p]);
+        } else {
+            const uint32_t r0 = ham_seeded<WORDS>(d0[2 * p], d1, seed);
+            const uint32_t r1 = ham_seeded<WORDS>(d0[2 * p + 1], d1, seed);
+            const uint32_t key = __builtin_amdgcn_perm(r1, r0, 0x04050001u);
+            lo[p] = pk_min_u16(lo[p], key);
+            if (NODUPES) hi[p] = pk_min_u16(hi[p], key ^ 0x00FF00FFu);
+        }
+    }
+}
+
+template <int WORDS, bool NODUPES, int RP, int STEP>
+__global__ __launch_bounds__(512) void search16_kernel(SearchArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
+
+    const int nwg = gridDim.x;
+    const int bid = blockIdx.x;
+    const int per_xcd = (nwg + 7) / 8;
+    int logical = (bid % 8) * per_xcd + bid / 8;
+    if (nwg % 8 != 0) logical = bid;
+    const int row = logical / a.tiles_per_row;
+    const int tile = logical % a.tiles_per_row;
+
+    constexpr int R = 2 * RP;
+    // waves = groups x split: the `split` waves of a group hold the same col0 and scan
+    // interleaved 256-column tiles of the right row; their minima merge through LDS.
+    const int split = a.split;
+    const int groups = blockDim.x / 64 / split;
+    const int wave = threadIdx.x / 64;
+    const int group = wave / split;
+    const int seg = wave % split;
+    const int lane = threadIdx.x % 64;
+    const int cols = a.cols;
+    const int col0_base = tile * groups * 64 * R + group * 64 * R + lane;
+    const uint32_t top_mask = WORDS == 8 ? 0x7FFFFFFFu : 0xFFFFFFFFu;
+
+    const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
+    const uint32_t* __restrict__ row1 = a.desc1 + (size_t)row * a.desc_pitch;
+
+    uint32_t d0[R][WORDS];
+    uint32_t glo[R], ghi[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int c0 = col0_base + r * 64;
+        const int cc = c0 < cols ? c0 : cols - 1;
+        lds_fetch<WORDS>(row0 + (size_t)cc * WORDS, d0[r]);
+        d0[r][WORDS - 1] &= top_mask;
+        glo[r] = 0xFFFFFFFFu;
+        ghi[r] = 0xFFFFFFFFu;
+    }
+
+    for (int base = 0; base < cols; base += a.chunk) {
+        const int ncols = min(a.chunk, cols - base);
+        const int nwords = ncols * WORDS;
+        if (base) __syncthreads();
+        {
+            const uint32_t* src = row1 + (size_t)base * WORDS;
+            const int n4 = nwords / 4;
+            for (int i = threadIdx.x; i < n4; i += blockDim.x) {
+                uint4 v = ((const uint4*)src)[i];
+                if (WORDS == 8 && (i & 1)) v.w &= top_mask;
+                ((uint4*)lds)[i] = v;
+            }
+            for (int i = n4 * 4 + threadIdx.x; i < nwords; i += blockDim.x) lds[i] = src[i];
+        }
+        __syncthreads();
+
+        for (int t0 = seg * 256; t0 < ncols; t0 += 256 * split) {
+            const int tn = min(256, ncols - t0);
+            uint32_t lo[RP], hi[RP];
+#pragma unroll
+            for (int p = 0; p < RP; ++p) {
+                lo[p] = 0xFFFFFFFFu;
+                hi[p] = 0xFFFFFFFFu;
+            }
+            const uint32_t* tl = lds + t0 * WORDS;
+            constexpr int U = WORDS >= 8 ? 4 : 8;
+            int j = 0;
+            for (; j + U <= tn; j += U) {
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    search16_step<WORDS, NODUPES, RP, STEP>(tl + (j + u) * WORDS,
+                                                            (uint32_t)(j + u) << 8, d0, lo, hi);
+            }
+            for (; j < tn; ++j)
+                search16_step<WORDS, NODUPES, RP, STEP>(tl + j * WORDS, (uint32_t)j << 8, d0, lo,
+                                                        hi);
+
+            // fold the tile's 16-bit keys into 32-bit (cost << 16 | col1) keys
+            const uint32_t tb = (uint32_t)(base + t0);
+#pragma unroll
+            for (int p = 0; p < RP; ++p) {
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const uint32_t v = (lo[p] >> (16 * h)) & 0xFFFFu;
+                    const uint32_t k = ((v >> 8) << 16) | (tb + (v & 0xFFu));
+                    glo[2 * p + h] = min(glo[2 * p + h], k);
+                    if (NODUPES) {
+                        const uint32_t w = (hi[p] >> (16 * h)) & 0xFFFFu;
+                        const uint32_t last = tb + 255u - (w & 0xFFu);
+                        const uint32_t kh = ((w >> 8) << 16) | (0xFFFFu - last);
+                        ghi[2 * p + h] = min(ghi[2 * p + h], kh);
+                    }
+                }
+            }
+        }
+    }
+
+    if (split > 1) {
+        // merge the segments' minima (min of disjoint col1 ranges is exact)
+        __syncthreads();
+        uint32_t* m = lds;  // the row stage is dead now
+        const int slot = (group * 64 + lane) * R;
+        if (seg > 0) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                m[((seg - 1) * groups * 64 * R + slot + r) * 2] = glo[r];
+                m[((seg - 1) * groups * 64 * R + slot + r) * 2 + 1] = ghi[r];
+            }
+        }
+        __syncthreads();
+        if (seg > 0) return;
+        for (int q = 0; q < split - 1; ++q)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                glo[r] = min(glo[r], m[(q * groups * 64 * R + slot + r) * 2]);
+                ghi[r] = min(ghi[r], m[(q * groups * 64 * R + slot + r) * 2 + 1]);
+            }
+    }
+
+    int16_t* __restrict__ out = a.out + (size_t)row * a.out_pitch;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const int c0 = col0_base + r * 64;
+        if (c0 >= cols) continue;
+        const int first = (int)(glo[r] & 0xFFFFu);
+        const bool dup = NODUPES && (int)(0xFFFFu - (ghi[r] & 0xFFFFu)) != first;
+        int16_t v;
+        if (a.out_mode == 0)
+            v = dup ? INVALID_I16 : (int16_t)(c0 - first);
+        else
+            v = dup ? (int16_t)-1 : (int16_t)first;
+        out[c0] = v;
+    }
+}
+
 // Left-right consistency (bicos.hpp:99-106): fwd[c0] = best col1 (or -1), rev[c1] = best
 // col0 of the reverse search (or -1).
 __global__ __launch_bounds__(256) void consistency_kernel(ConsistencyArgs a) {
@@ -323,7 +666,25 @@ __device__ __forceinline__ float fma_p(float a, float b, float c) { return __bui
 __device__ __forceinline__ double fma_p(double a, double b, double c) { return __builtin_fma(a, b, c); }
 __device__ __forceinline__ float div_p(float a, float b) { return __fdiv_rn(a, b); }
 __device__ __forceinline__ double div_p(double a, double b) { return __ddiv_rn(a, b); }
-__device__ __forceinline__ float sqrt_p(float a) { return __fsqrt_rn(a); }
+// Correctly rounded sqrtf. hipcc lowers __fsqrt_rn / sqrtf to a bare v_sqrt_f32 (up to
+// 1 ulp off) here; the reference's std::sqrt is IEEE. Fix the estimate s with the residuals
+// of its two float neighbours (x - s_dn*s <= 0 -> s_dn; x - s_up*s > 0 -> s_up), after
+// scaling tiny inputs into the normal range.
+__device__ __forceinline__ float sqrt_p(float x) {
+    const bool tiny = x < 0x1.0p-96f;
+    const float xs = tiny ? x * 0x1.0p+32f : x;
+    float s = __builtin_amdgcn_sqrtf(xs);
+    const int si = __float_as_int(s);
+    const float s_dn = __int_as_float(si - 1);
+    const float s_up = __int_as_float(si + 1);
+    const float r_dn = __builtin_fmaf(-s_dn, s, xs);
+    const float r_up = __builtin_fmaf(-s_up, s, xs);
+    s = r_dn <= 0.f ? s_dn : s;
+    s = r_up > 0.f ? s_up : s;
+    s = tiny ? s * 0x1.0p-16f : s;
+    // zero, +inf and NaN (and negative) pass through the hardware result
+    return (xs == 0.f || xs == __builtin_inff() || !(xs > 0.f)) ? __builtin_amdgcn_sqrtf(x) : s;
+}
 __device__ __forceinline__ double sqrt_p(double a) { return __dsqrt_rn(a); }
 
 // nxcorr (agree.hpp:28-51): means from exact integer sums (< 2^24, identical to the
@@ -371,6 +732,61 @@ __global__ __launch_bounds__(256) void agree_kernel(AgreeArgs a) {
             const TIn* s1 = (const TIn*)a.stack1 + (size_t)row * a.row_pitch;
             corr = nxcorr_dev<TIn, TPrec>(s0 + col, s1 + idx1, a.plane_pitch, a.n, a.has_minvar,
                                           (TPrec)a.minvar);
+            if (corr < (TPrec)a.threshold) d = INVALID_I16;  // NaN passes, as in the reference
+        }
+    }
+    if (a.out_f32)
+        ((float*)a.out)[o] = (float)d;
+    else
+        ((int16_t*)a.out)[o] = (int16_t)d;
+    if (a.corrmap) ((TPrec*)a.corrmap)[o] = corr;
+}
+
+// agree with the 2n samples loaded once into registers (MAXN >= n), the same arithmetic
+// and output contract as agree_kernel.
+template <typename TIn, typename TPrec, int MAXN>
+__global__ __launch_bounds__(256) void agree_reg_kernel(AgreeArgs a) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    const int row = blockIdx.y;
+    if (col >= a.cols) return;
+    const size_t o = (size_t)row * a.cols + col;
+    int d = a.raw[(size_t)row * a.raw_pitch + col];
+    TPrec corr = (TPrec)__builtin_nan("");
+    if (d != INVALID_I16) {
+        const int idx1 = col - d;
+        if (idx1 < 0 || idx1 >= a.cols) {
+            d = INVALID_I16;
+        } else {
+            const int n = a.n;
+            const size_t pp = a.plane_pitch;
+            const TIn* s0 = (const TIn*)a.stack0 + (size_t)row * a.row_pitch + col;
+            const TIn* s1 = (const TIn*)a.stack1 + (size_t)row * a.row_pitch + idx1;
+            uint32_t l[MAXN], r[MAXN];
+            uint32_t sl = 0, sr = 0;
+#pragma unroll
+            for (int t = 0; t < MAXN; ++t)
+                if (t < n) {
+                    l[t] = ld(s0 + t * pp);
+                    r[t] = ld(s1 + t * pp);
+                    sl += l[t];
+                    sr += r[t];
+                }
+            const TPrec m0 = div_p((TPrec)sl, (TPrec)n);
+            const TPrec m1 = div_p((TPrec)sr, (TPrec)n);
+            TPrec cov = 0, v0 = 0, v1 = 0;
+#pragma unroll
+            for (int t = 0; t < MAXN; ++t)
+                if (t < n) {
+                    const TPrec x0 = (TPrec)l[t] - m0;
+                    const TPrec x1 = (TPrec)r[t] - m1;
+                    cov = fma_p(x0, x1, cov);
+                    v0 = fma_p(x0, x0, v0);
+                    v1 = fma_p(x1, x1, v1);
+                }
+            if (a.has_minvar && (v0 < (TPrec)a.minvar || v1 < (TPrec)a.minvar))
+                corr = (TPrec)-1;
+            else
+                corr = div_p(cov, sqrt_p(v0 * v1));
             if (corr < (TPrec)a.threshold) d = INVALID_I16;  // NaN passes, as in the reference
         }
     }
@@ -477,13 +893,28 @@ __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
 
 // ------------------------------------------------------------------- dispatch
 
+template <typename TIn, int WORDS, int MAXN>
+hipError_t launch_tl(const TransformArgs& a, dim3 grid, hipStream_t st) {
+    hipLaunchKernelGGL((transform_limited_kernel<TIn, WORDS, MAXN>), grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 template <typename TIn, int WORDS>
 hipError_t launch_transform_w(const TransformArgs& a, int mode, hipStream_t st) {
     dim3 grid((a.cols + 255) / 256, a.rows, a.stack1 ? 2 : 1);
-    if (mode == 0)
-        hipLaunchKernelGGL((transform_kernel<TIn, WORDS, 0>), grid, dim3(256), 0, st, a);
-    else
-        hipLaunchKernelGGL((transform_kernel<TIn, WORDS, 1>), grid, dim3(256), 0, st, a);
+    if (mode == 0) {
+        // descriptor width bounds n: 32 bits -> n <= 9, 64 -> 17, 128 -> 33, 256 -> 65
+        const int n = a.n;
+        if (WORDS == 1) return launch_tl<TIn, WORDS, 9>(a, grid, st);
+        if (WORDS == 2) return n <= 12 ? launch_tl<TIn, WORDS, 12>(a, grid, st)
+                                       : launch_tl<TIn, WORDS, 17>(a, grid, st);
+        if (WORDS == 4) return n <= 24 ? launch_tl<TIn, WORDS, 24>(a, grid, st)
+                                       : launch_tl<TIn, WORDS, 33>(a, grid, st);
+        if (n <= 40) return launch_tl<TIn, WORDS, 40>(a, grid, st);
+        if (n <= 48) return launch_tl<TIn, WORDS, 48>(a, grid, st);
+        return launch_tl<TIn, WORDS, 65>(a, grid, st);
+    }
+    hipLaunchKernelGGL((transform_kernel<TIn, WORDS, 1>), grid, dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
@@ -506,20 +937,45 @@ hipError_t launch_search_r(const SearchArgs& a, int waves, hipStream_t st) {
     return hipGetLastError();
 }
 
+template <int WORDS, bool NODUPES, int RP, int STEP>
+hipError_t launch_search16_r(const SearchArgs& a, int waves, hipStream_t st) {
+    const size_t stage = (size_t)a.chunk * WORDS * 4;
+    const size_t merge = a.split > 1 ? (size_t)(waves / a.split) * 64 * (2 * RP) * 8 * (a.split - 1) : 0;
+    const size_t lds = stage > merge ? stage : merge;
+    const int nwg = a.rows * a.tiles_per_row;
+    hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP, STEP>), dim3(nwg), dim3(64 * waves), lds,
+                       st, a);
+    return hipGetLastError();
+}
+
 template <int WORDS, bool NODUPES>
-hipError_t launch_search_n(const SearchArgs& a, int R, int waves, hipStream_t st) {
-    switch (R) {
-        case 1: return launch_search_r<WORDS, NODUPES, 1>(a, waves, st);
-        case 2: return launch_search_r<WORDS, NODUPES, 2>(a, waves, st);
-        case 4: return launch_search_r<WORDS, NODUPES, 4>(a, waves, st);
+hipError_t launch_search_n(const SearchArgs& a, const SearchGeometry& g, hipStream_t st) {
+    if (g.variant == 16) {
+        switch (g.R) {
+            case 2: return launch_search16_r<WORDS, NODUPES, 1, 0>(a, g.waves, st);
+            case 4: return launch_search16_r<WORDS, NODUPES, 2, 0>(a, g.waves, st);
+        }
+        return hipErrorInvalidValue;
+    }
+    if (g.variant == 17) {
+        switch (g.R) {
+            case 2: return launch_search16_r<WORDS, NODUPES, 1, 1>(a, g.waves, st);
+            case 4: return launch_search16_r<WORDS, NODUPES, 2, 1>(a, g.waves, st);
+        }
+        return hipErrorInvalidValue;
+    }
+    switch (g.R) {
+        case 1: return launch_search_r<WORDS, NODUPES, 1>(a, g.waves, st);
+        case 2: return launch_search_r<WORDS, NODUPES, 2>(a, g.waves, st);
+        case 4: return launch_search_r<WORDS, NODUPES, 4>(a, g.waves, st);
     }
     return hipErrorInvalidValue;
 }
 
 template <int WORDS>
-hipError_t launch_search_w(const SearchArgs& a, bool nodupes, int R, int waves, hipStream_t st) {
-    return nodupes ? launch_search_n<WORDS, true>(a, R, waves, st)
-                   : launch_search_n<WORDS, false>(a, R, waves, st);
+hipError_t launch_search_w(const SearchArgs& a, bool nodupes, const SearchGeometry& g,
+                           hipStream_t st) {
+    return nodupes ? launch_search_n<WORDS, true>(a, g, st) : launch_search_n<WORDS, false>(a, g, st);
 }
 
 template <typename TIn, typename TPrec, int MAXN>
@@ -543,8 +999,24 @@ hipError_t launch_subpixel_t(const AgreeArgs& a, hipStream_t st) {
     return hipErrorInvalidValue;
 }
 
+template <typename TIn, typename TPrec, int MAXN>
+hipError_t launch_agree_m(const AgreeArgs& a, hipStream_t st) {
+    dim3 grid((a.cols + 255) / 256, a.rows);
+    hipLaunchKernelGGL((agree_reg_kernel<TIn, TPrec, MAXN>), grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
 template <typename TIn, typename TPrec>
 hipError_t launch_agree_t(const AgreeArgs& a, hipStream_t st) {
+    const int n = a.n;
+    if (n <= 8) return launch_agree_m<TIn, TPrec, 8>(a, st);
+    if (n <= 16) return launch_agree_m<TIn, TPrec, 16>(a, st);
+    if (n <= 24) return launch_agree_m<TIn, TPrec, 24>(a, st);
+    if (n <= 33) return launch_agree_m<TIn, TPrec, 33>(a, st);
+    if (n <= 40) return launch_agree_m<TIn, TPrec, 40>(a, st);
+    if (n <= 48) return launch_agree_m<TIn, TPrec, 48>(a, st);
+    if (n <= 65) return launch_agree_m<TIn, TPrec, 65>(a, st);
+    // beyond the descriptor limit only the stage API can get here: generic kernel
     dim3 grid((a.cols + 255) / 256, a.rows);
     hipLaunchKernelGGL((agree_kernel<TIn, TPrec>), grid, dim3(256), 0, st, a);
     return hipGetLastError();
@@ -561,20 +1033,34 @@ hipError_t launch_transform(const TransformArgs& a, int depth, int mode, int wor
                       : launch_transform_t<uint16_t>(a, mode, words, st);
 }
 
-SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes) {
+SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes, int variant,
+                               int R, int waves, int split) {
     SearchGeometry g;
+    g.variant = (variant == 32 || variant == 17) ? variant : 16;
     // col1 chunk staged per LDS fill: the whole row when it fits
     const int max_chunk = max_lds_bytes / (words * 4);
     g.chunk = cols < max_chunk ? cols : max_chunk;
-    // register blocking and waves: enough workgroups to cover 256 CUs several times
-    g.waves = 4;
-    g.R = 2;
-    const long per_wg = 64L * g.waves * g.R;
-    long tiles = (cols + per_wg - 1) / per_wg;
-    if ((long)rows * tiles < 1024) {
-        g.R = 1;
+    // 8 waves per workgroup: the row stage (<= 64 KiB) caps resident workgroups per CU,
+    // so wide workgroups are what fill the 32 wave slots (measured: 4 waves -1 %, 2 waves
+    // +40 % time at cfg2)
+    g.waves = waves ? waves : 8;
+    g.R = R ? R : 2;
+    if (g.variant == 32) {
+        g.split = 1;
+    } else if (split) {
+        g.split = split;
+    } else {
+        // split the col1 scan across waves until ~32 waves per CU are in flight
+        const long base = (long)rows * ((cols + 64L * g.R - 1) / (64L * g.R));
+        const int tiles256 = (cols + 255) / 256;
+        g.split = 1;
+        // measured best: cfg2 full frame split 2, 192-row band split 4, 270x3840 split 4
+        while (g.split < 4 && base * g.split < 256L * 128 && tiles256 >= 2 * g.split &&
+               g.waves % (2 * g.split) == 0)
+            g.split *= 2;
     }
-    g.tiles_per_row = (int)((cols + 64L * g.waves * g.R - 1) / (64L * g.waves * g.R));
+    const long per_wg = 64L * (g.waves / g.split) * g.R;
+    g.tiles_per_row = (int)((cols + per_wg - 1) / per_wg);
     return g;
 }
 
@@ -583,11 +1069,13 @@ hipError_t launch_search(SearchArgs a, const SearchGeometry& g, int words, bool 
     if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
     a.chunk = g.chunk;
     a.tiles_per_row = g.tiles_per_row;
+    a.split = g.split;
+    if (g.waves % g.split) return hipErrorInvalidValue;
     switch (words) {
-        case 1: return launch_search_w<1>(a, nodupes, g.R, g.waves, st);
-        case 2: return launch_search_w<2>(a, nodupes, g.R, g.waves, st);
-        case 4: return launch_search_w<4>(a, nodupes, g.R, g.waves, st);
-        case 8: return launch_search_w<8>(a, nodupes, g.R, g.waves, st);
+        case 1: return launch_search_w<1>(a, nodupes, g, st);
+        case 2: return launch_search_w<2>(a, nodupes, g, st);
+        case 4: return launch_search_w<4>(a, nodupes, g, st);
+        case 8: return launch_search_w<8>(a, nodupes, g, st);
     }
     return hipErrorInvalidValue;
 }

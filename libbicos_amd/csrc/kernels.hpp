@@ -29,6 +29,7 @@ struct SearchArgs {
     int out_mode;           // 0: disparity col0-best (INVALID -32768), 1: best index (-1)
     int chunk;              // set by launch_search
     int tiles_per_row;      // set by launch_search
+    int split;              // set by launch_search: waves per col0 group scanning col1 tiles
 };
 
 struct SearchGeometry {
@@ -36,6 +37,8 @@ struct SearchGeometry {
     int waves;              // waves per workgroup
     int R;                  // col0 per lane
     int tiles_per_row;
+    int variant;            // 16: packed 16-bit keys (default), 32: 32-bit keys
+    int split;              // packed variant: col1 split across waves of a workgroup (1, 2, 4)
 };
 
 struct ConsistencyArgs {
@@ -64,7 +67,8 @@ struct AgreeArgs {
 };
 
 hipError_t launch_transform(const TransformArgs& a, int depth, int mode, int words, hipStream_t st);
-SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes);
+SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes, int variant = 16,
+                               int R = 0, int waves = 0, int split = 0);
 hipError_t launch_search(SearchArgs a, const SearchGeometry& g, int words, bool nodupes,
                          hipStream_t st);
 hipError_t launch_consistency(const ConsistencyArgs& a, hipStream_t st);

@@ -96,6 +96,12 @@ class Engine:
         except Exception:
             pass
 
+    def tune(self, variant: int = 0, col0_per_lane: int = 0, waves: int = 0,
+             split: int = 0) -> None:
+        """Search-kernel variant / register blocking / waves / col1 split (0 = automatic)."""
+        _lib.check(self._L.bicos_engine_tune(self._h, variant, col0_per_lane, waves, split),
+                   "bicos_engine_tune")
+
     # ------------------------------------------------------------------ match
     def match(self, stack0: torch.Tensor, stack1: torch.Tensor,
               cfg: Optional[MatchConfig] = None, want_corrmap: bool = True,

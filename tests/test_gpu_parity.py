@@ -335,3 +335,28 @@ def test_deterministic(gpu):
     b = gpu_match(gpu, L, R, nxcorr_threshold=0.9, subpixel_step=0.1)
     same(a[0], b[0])
     same(a[1], b[1])
+
+
+@pytest.mark.parametrize("words", [1, 2, 4, 8])
+def test_search_tuning_settings_are_exact(gpu, oracle, words):
+    """Every (variant, col0/lane, waves, col1-split) produces the oracle's result."""
+    H, W = 6, 1100
+    rng = np.random.default_rng(words)
+    a = rng.integers(0, 2 ** 32, size=(H, W, words), dtype=np.uint64).astype(np.uint32)
+    b = a[:, np.roll(np.arange(W), 7)] ^ (rng.random((H, W, words)) < 0.03).astype(np.uint32)
+    if words == 8:   # descriptors from the transform never use bit 255 (4n-6 <= 254)
+        a[..., 7] &= 0x7FFFFFFF
+        b[..., 7] &= 0x7FFFFFFF
+    lo = _low_entropy_desc(H, W, words, 3)
+    settings = [(32, 1, 4, 0), (32, 2, 8, 0), (32, 4, 2, 0), (16, 2, 8, 1), (16, 2, 8, 2),
+                (16, 2, 8, 4), (16, 4, 4, 2), (16, 4, 8, 4), (16, 2, 1, 1), (16, 2, 2, 2)]
+    try:
+        for flags, lr in ((1, -1), (3, 1), (2, 2)):
+            for (x, y) in ((a, b), (lo, lo[:, ::-1].copy())):
+                ref = oracle.search(x, y, flags, lr)
+                for s in settings:
+                    gpu.tune(*s)
+                    out = host(gpu.search(dev(_pack(x)), dev(_pack(y)), W, words, flags, lr))
+                    same(out, ref)
+    finally:
+        gpu.tune(0, 0, 0, 0)

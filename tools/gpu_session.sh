@@ -1,0 +1,34 @@
+#!/bin/bash
+# One gpurun session: each GPU step has its own time limit; stop at the first
+# crash/timeout (exit >= 2 other than pytest's 1 = test failures).
+set -u
+mkdir -p gpurun_out
+run() {  # name timeout cmd...
+    local name=$1 to=$2; shift 2
+    echo "=== $name: $*" | tee -a gpurun_out/session.log
+    timeout -k 10 "$to" "$@" > "gpurun_out/$name.txt" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc" | tee -a gpurun_out/session.log
+    tail -3 "gpurun_out/$name.txt" | tee -a gpurun_out/session.log
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "STOP after $name (rc=$rc)" | tee -a gpurun_out/session.log; exit $rc; fi
+    return 0
+}
+for step in "$@"; do
+    case $step in
+        valu) run valu 120 ./build/valu_peak ;;
+        smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
+        pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+        pytestk) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
+        bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
+        bench3) run bench3 600 python bench.py --config cfg3 --steps 10 --warmup 2 --no-cpu-baseline ;;
+        bench4) run bench4 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline ;;
+        bench5) run bench5 600 python bench.py --config cfg5 --steps 10 --warmup 2 --no-cpu-baseline ;;
+        sweep) run sweep 600 python tools/search_sweep.py --variants 16:2:8:1,17:2:8:1,16:2:8:2,17:2:8:2,16:4:8:1,17:4:8:1 ;;
+        sweep4) run sweep4 600 python tools/search_sweep.py --config cfg4 --variants 0:0:0:0,32:2:4,16:2:8:1,16:4:8:1,16:2:8:2 ;;
+        sweep1) run sweep1 600 python tools/search_sweep.py --config cfg1 --variants 32:1:4,32:2:4,16:2:4,16:4:4,16:2:2,16:2:1 ;;
+        sweep8) run sweep8 600 python tools/search_sweep.py --rows 192 --variants 16:2:8:4,17:2:8:4,16:4:8:4,17:4:8:4,16:2:8:2,17:2:8:2 ;;
+        sweep5) run sweep5 600 python tools/search_sweep.py --config cfg5 --rows 270 --variants 0:0:0:0,16:2:8:1,16:2:8:2,16:2:8:4 ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+        *) echo "unknown step $step" ;;
+    esac
+done

@@ -27,6 +27,31 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
             if (OP == 2) asm volatile("v_min_u32 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
             if (OP == 3) asm volatile("v_med3_u32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
             if (OP == 4) asm volatile("v_lshl_or_b32 %0, %0, 16, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 5) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "s"(0x05010400u));
+            if (OP == 6) asm volatile("v_pk_min_u16 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 7) asm volatile("v_pk_max_u16 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 8) asm volatile("v_and_b32 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 9) asm volatile("v_add_u32 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 10) asm volatile("v_min3_u32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
+            if (OP == 11) asm volatile("v_xor_b32_e64 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 12) asm volatile("v_min_u32_e64 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 13) asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(v[c]) : "s"(seed));
+            if (OP == 14) asm volatile("v_mov_b32 %0, %1" : "=v"(v[c]) : "v"(w[c]));
+            if (OP == 15) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
+            if (OP == 16) {  // the search loop's 128-bit mix per pair: 4 xor, 4 bcnt, lshl_or, med3, min
+                uint32_t t0, t1, t2, t3, cst, key;
+                asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t0) : "v"(v[c]), "v"(w[c]));
+                asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t1) : "v"(v[c]), "v"(w[(c + 1) % CHAINS]));
+                asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t2) : "v"(v[c]), "v"(w[(c + 2) % CHAINS]));
+                asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t3) : "v"(v[c]), "v"(w[(c + 3) % CHAINS]));
+                asm volatile("v_bcnt_u32_b32 %0, %1, 0" : "=v"(cst) : "v"(t0));
+                asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(cst) : "v"(t1));
+                asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(cst) : "v"(t2));
+                asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(cst) : "v"(t3));
+                asm volatile("v_lshl_or_b32 %0, %1, 16, %2" : "=v"(key) : "v"(cst), "s"(i));
+                asm volatile("v_med3_u32 %0, %1, %2, %0" : "+v"(w[(c + 4) % CHAINS]) : "v"(v[c]), "v"(key));
+                asm volatile("v_min_u32 %0, %0, %1" : "+v"(v[c]) : "v"(key));
+            }
         }
     }
     uint32_t r = 0;
@@ -52,7 +77,7 @@ double run(const char* name, uint32_t* out, int grid) {
         hipEventElapsedTime(&ms, a, b);
         if (ms < best) best = ms;
     }
-    const double ops = (double)grid * 256 * ITERS * CHAINS;  // lane-ops
+    const double ops = (double)grid * 256 * ITERS * CHAINS * (OP == 16 ? 11 : 1);  // lane-ops
     const double tops = ops / (best * 1e-3) / 1e12;
     printf("{\"op\": \"%s\", \"lane_ops\": %.3e, \"ms\": %.4f, \"Tops\": %.2f}\n", name, ops, best, tops);
     return tops;
@@ -75,6 +100,18 @@ int main() {
     run<2>("v_min_u32", out, grid);
     run<3>("v_med3_u32", out, grid);
     run<4>("v_lshl_or_b32", out, grid);
+    run<5>("v_perm_b32", out, grid);
+    run<6>("v_pk_min_u16", out, grid);
+    run<7>("v_pk_max_u16", out, grid);
+    run<8>("v_and_b32", out, grid);
+    run<9>("v_add_u32", out, grid);
+    run<10>("v_min3_u32", out, grid);
+    run<11>("v_xor_b32_e64", out, grid);
+    run<12>("v_min_u32_e64", out, grid);
+    run<13>("v_bcnt_u32_b32(sgpr)", out, grid);
+    run<14>("v_mov_b32", out, grid);
+    run<15>("v_xad_u32", out, grid);
+    run<16>("search_mix_128(11 ops/pair)", out, grid);
     hipFree(out);
     return 0;
 }
