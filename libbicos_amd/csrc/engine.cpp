@@ -84,6 +84,21 @@ bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, in
 
 static int required_bits(int n, int mode) { return mode ? n * n - 2 * n + 3 : 4 * n - 7; }
 
+// Bytes the kernels may address from a stack base; the kernels use 32-bit buffer offsets.
+static int stack_span(int n, int rows, int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                      uint32_t* out) {
+    if (rows <= 0 || cols <= 0) {
+        *out = 0;
+        return BICOS_OK;
+    }
+    const unsigned long long span =
+        ((unsigned long long)(n - 1) * plane_pitch + (unsigned long long)(rows - 1) * row_pitch +
+         (unsigned long long)cols) * (unsigned long long)depth;
+    if (span > 0xFFFFFFFFull) return fail(BICOS_E_ARG, "image stack spans more than 4 GiB");
+    *out = (uint32_t)span;
+    return BICOS_OK;
+}
+
 int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int rows, int cols,
                  size_t row_pitch, size_t plane_pitch, int depth, const BicosConfig& cfg,
                  bool has_nxcorr, float threshold, void* disp, void* corr, hipStream_t st) {
@@ -108,6 +123,8 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     if (!s0 || !s1 || !disp) return fail(BICOS_E_ARG, "null buffer");
     if (row_pitch < (size_t)cols || plane_pitch < (size_t)rows * row_pitch)
         return fail(BICOS_E_ARG, "row/plane pitch smaller than the image");
+    uint32_t span = 0;
+    if (int rc0 = stack_span(n, rows, cols, row_pitch, plane_pitch, depth, &span)) return rc0;
 
     const bool consistency = cfg.variant_type != 0;
     const bool nodupes = consistency ? cfg.no_dupes != 0 : true;
@@ -131,7 +148,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     int16_t* rev = consistency ? (int16_t*)(p + map16) : nullptr;
 
     // 1. descriptor_transform, both stacks in one launch (cpu.cpp:50-59)
-    bicos_hip::TransformArgs ta{s0, s1, d0, d1, n, rows, cols, row_pitch, plane_pitch, dpitch};
+    bicos_hip::TransformArgs ta{s0, s1, d0, d1, n, rows, cols, row_pitch, plane_pitch, dpitch, 0, span};
     rc = check_hip(bicos_hip::launch_transform(ta, depth, mode, words, st), "transform launch");
     if (rc) return rc;
 
@@ -172,6 +189,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     aa.out = disp;
     aa.out_f32 = 1;
     aa.corrmap = corr;
+    aa.stack_bytes = span;
     if (has_step)
         rc = check_hip(bicos_hip::launch_subpixel(aa, depth, dbl, st), "subpixel launch");
     else
@@ -305,8 +323,10 @@ int bicos_transform_device(const void* stack, int n, int rows, int cols, size_t 
         return fail(BICOS_E_ARG, "words must be 1, 2, 4 or 8");
     const int need = descriptor_words(n, mode ? 1 : 0);
     if (need < 0 || need > words) return fail(BICOS_E_BITS, "descriptor too narrow for n");
+    uint32_t span = 0;
+    if (int rc0 = stack_span(n, rows, cols, row_pitch, plane_pitch, depth, &span)) return rc0;
     bicos_hip::TransformArgs ta{stack, nullptr, desc, nullptr, n, rows, cols,
-                                row_pitch, plane_pitch, bicos_desc_pitch(cols, words)};
+                                row_pitch, plane_pitch, bicos_desc_pitch(cols, words), 0, span};
     return check_hip(bicos_hip::launch_transform(ta, depth, mode ? 1 : 0, words, (hipStream_t)stream),
                      "transform launch");
 }
@@ -368,6 +388,7 @@ static int agree_common(bool sub, const int16_t* raw, const void* stack0, const 
     aa.out = out;
     aa.out_f32 = 1;
     aa.corrmap = corrmap;
+    if (int rc0 = stack_span(n, rows, cols, row_pitch, plane_pitch, depth, &aa.stack_bytes)) return rc0;
     hipStream_t st = (hipStream_t)stream;
     return sub ? check_hip(bicos_hip::launch_subpixel(aa, depth, false, st), "subpixel launch")
                : check_hip(bicos_hip::launch_agree(aa, depth, false, st), "agree launch");

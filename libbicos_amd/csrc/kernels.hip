@@ -47,6 +47,23 @@ __device__ __forceinline__ uint32_t ld(const T* p) {
     return (uint32_t)__builtin_nontemporal_load(p);
 }
 
+// Raw buffer loads of an image stack: 128-bit resource built from uniform values, uniform
+// (SGPR) byte offset of the plane/row, 32-bit per-lane byte offset -- no VALU address math
+// per load (guide T8). Stacks are limited to < 4 GiB (checked by the engine).
+template <typename TIn>
+struct StackReader {
+    __amdgpu_buffer_rsrc_t r;
+    __device__ __forceinline__ StackReader(const void* base, uint32_t bytes)
+        : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
+                                               0x00020000)) {}
+    __device__ __forceinline__ uint32_t operator()(uint32_t lane_elem, uint32_t uniform_elem) const {
+        if constexpr (sizeof(TIn) == 1)
+            return __builtin_amdgcn_raw_buffer_load_b8(r, lane_elem, uniform_elem, 0);
+        else
+            return __builtin_amdgcn_raw_buffer_load_b16(r, lane_elem * 2u, uniform_elem * 2u, 0);
+    }
+};
+
 // ------------------------------------------------------------------ transform
 
 // Sequential bit writer: bit i of the descriptor is the i-th comparison, LSB first
@@ -167,64 +184,148 @@ __global__ __launch_bounds__(256) void transform_kernel(TransformArgs a) {
     }
 }
 
-// LIMITED transform with the n samples of a pixel held in registers (MAXN >= n bounds
-// the static arrays; t >= n slots are skipped by wave-uniform branches) and every loop
-// bit at a compile-time position: t = 0, 1 emit bits 3t..3t+2, t >= 2 emits bits
-// 6+4(t-2) .. 9+4(t-2) (a<b, a<c, a<av, ps[t-2]<ps[t]); only the 4 tail bits land at an
-// n-dependent position. One load per sample (the two-pass kernel above re-reads them).
-template <typename TIn, int WORDS, int MAXN>
+// LIMITED transform, one pixel per lane, the n samples held in registers (MAXN >= n bounds
+// the static arrays; slots t >= n are skipped by wave-uniform branches).
+//
+// Bits are pushed MSB-first into `cur` with v_cmp (-> an SGPR lane mask) + v_addc
+// (cur = 2*cur + bit): 2 full-rate VALU per bit. Each asm block issues all its compares
+// before its adds, so every mask is read >= 2 instructions after it is written (the VALU
+// SGPR-write -> carry-read spacing hipcc itself pads with s_nop 1 on gfx950). Loop bits sit
+// at compile-time positions (t = 0, 1: 3t..3t+2; t >= 2: 6+4(t-2)..9+4(t-2)) because the
+// per-t steps are unrolled by template recursion, so the 32-bit flushes (v_bfrev back to
+// the reference's LSB-first order) are static; only the 4 tail bits and the last partial
+// word land at n-dependent positions.
+//
+// `a < av` (float mean, descriptor_transform.hpp:36-39) is evaluated as `a < ceil(sum/n)`:
+// for integer a, a < RN(sum/n) <=> a*n < sum (the margin 1/n exceeds half an ulp of any
+// value <= 65535) <=> a < ceil(sum/n). ceil(sum/n) = q + (q*n != sum) with
+// q = umulhi(sum, magic), magic = ceil(2^32/n): exact because sum < 2^24 makes the
+// reciprocal's error < 2^-8 < 1/n (n <= 65).
+#define BICOS_CMP(i) "v_cmp_lt_u32_e64 %[m" #i "], %[x" #i "], %[y" #i "]\n\t"
+#define BICOS_ADD(i) "v_addc_co_u32_e64 %[c], %[j], %[c], %[c], %[m" #i "]\n\t"
+#define BICOS_M(i) [m##i] "=&s"(m##i)
+#define BICOS_XY(i) [x##i] "v"(x[i]), [y##i] "v"(y[i])
+
+template <int K>
+__device__ __forceinline__ void push_lt(uint32_t& cur, const uint32_t (&x)[4], const uint32_t (&y)[4]) {
+    uint64_t m0, m1, m2, m3, j;
+    if constexpr (K == 4)
+        asm(BICOS_CMP(0) BICOS_CMP(1) BICOS_CMP(2) BICOS_CMP(3) BICOS_ADD(0) BICOS_ADD(1)
+                BICOS_ADD(2) BICOS_ADD(3)
+            : [c] "+v"(cur), BICOS_M(0), BICOS_M(1), BICOS_M(2), BICOS_M(3), [j] "=&s"(j)
+            : BICOS_XY(0), BICOS_XY(1), BICOS_XY(2), BICOS_XY(3));
+    else if constexpr (K == 3)
+        asm(BICOS_CMP(0) BICOS_CMP(1) BICOS_CMP(2) BICOS_ADD(0) BICOS_ADD(1) BICOS_ADD(2)
+            : [c] "+v"(cur), BICOS_M(0), BICOS_M(1), BICOS_M(2), [j] "=&s"(j)
+            : BICOS_XY(0), BICOS_XY(1), BICOS_XY(2));
+    else if constexpr (K == 2)
+        asm(BICOS_CMP(0) BICOS_CMP(1) "s_nop 0\n\t" BICOS_ADD(0) BICOS_ADD(1)
+            : [c] "+v"(cur), BICOS_M(0), BICOS_M(1), [j] "=&s"(j)
+            : BICOS_XY(0), BICOS_XY(1));
+    else if constexpr (K == 1)
+        asm(BICOS_CMP(0) "s_nop 1\n\t" BICOS_ADD(0)
+            : [c] "+v"(cur), BICOS_M(0), [j] "=&s"(j)
+            : BICOS_XY(0));
+    (void)m0; (void)m1; (void)m2; (void)m3; (void)j;
+}
+#undef BICOS_CMP
+#undef BICOS_ADD
+#undef BICOS_M
+#undef BICOS_XY
+
+// Shift the comparisons x[i] < y[i], i < K, into the descriptor at static bit position POS.
+template <int POS, int K, int WORDS>
+__device__ __forceinline__ void emit_bits(uint32_t& cur, uint32_t (&w)[WORDS], const uint32_t (&x)[4],
+                                          const uint32_t (&y)[4]) {
+    constexpr int room = 32 - POS % 32;
+    if constexpr (K <= room) {
+        push_lt<K>(cur, x, y);
+        if constexpr (K == room) {
+            w[POS / 32] = __builtin_bitreverse32(cur);
+            cur = 0;
+        }
+    } else {
+        push_lt<room>(cur, x, y);
+        w[POS / 32] = __builtin_bitreverse32(cur);
+        cur = 0;
+        uint32_t x2[4] = {0, 0, 0, 0}, y2[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int i = room; i < K; ++i) {
+            x2[i - room] = x[i];
+            y2[i - room] = y[i];
+        }
+        push_lt<K - room>(cur, x2, y2);
+    }
+}
+
+template <int T, int MAXN, int WORDS>
+__device__ __forceinline__ void limited_steps(int n, uint32_t thr, const uint32_t (&v)[MAXN],
+                                              uint32_t& cur, uint32_t (&w)[WORDS]) {
+    if constexpr (T < MAXN - 2) {
+        if (T < n - 2) {
+            constexpr int pos = T < 2 ? 3 * T : 6 + 4 * (T - 2);
+            const uint32_t a = v[T], b = v[T + 1], c = v[T + 2];
+            if constexpr (T < 2) {
+                const uint32_t x[4] = {a, a, a, 0}, y[4] = {b, c, thr, 0};
+                emit_bits<pos, 3, WORDS>(cur, w, x, y);
+            } else {
+                // ps[t-2] < ps[t]  (descriptor_transform.hpp:52-58; ring slot t % 2)
+                const uint32_t x[4] = {a, a, a, v[T - 2] + v[T - 1]}, y[4] = {b, c, thr, a + b};
+                emit_bits<pos, 4, WORDS>(cur, w, x, y);
+            }
+            limited_steps<T + 1, MAXN, WORDS>(n, thr, v, cur, w);
+        }
+    }
+}
+
+template <typename TIn, int WORDS, int MAXN, bool EXACT>
 __global__ __launch_bounds__(256) void transform_limited_kernel(TransformArgs a) {
     const int col = blockIdx.x * 256 + threadIdx.x;
     const int row = blockIdx.y;
     const int which = blockIdx.z;
     if (col >= a.cols) return;
-    const TIn* __restrict__ p = (const TIn*)(which ? a.stack1 : a.stack0) + (size_t)row * a.row_pitch + col;
+    const StackReader<TIn> rd(which ? a.stack1 : a.stack0, a.stack_bytes);
     uint32_t* __restrict__ out = (which ? a.desc1 : a.desc0) + (size_t)row * a.desc_pitch + (size_t)col * WORDS;
-    const size_t pp = a.plane_pitch;
-    const int n = a.n;
+    const uint32_t pp = (uint32_t)a.plane_pitch;
+    const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
+    // EXACT: n == MAXN, so every `t < n` below is a compile-time constant
+    const int n = EXACT ? MAXN : a.n;
 
     uint32_t v[MAXN];
     uint32_t sum = 0;
 #pragma unroll
     for (int t = 0; t < MAXN; ++t)
         if (t < n) {
-            v[t] = ld(p + t * pp);
+            v[t] = rd((uint32_t)col, rowoff + (uint32_t)t * pp);
             sum += v[t];
         }
-    // exact: integer sum == the reference's sequential float sum (< 2^24)
-    const float av = fdiv_rn((float)sum, (float)n);
+    const uint32_t q = __umulhi(sum, a.magic);
+    const uint32_t thr = q + (q * (uint32_t)n != sum ? 1u : 0u);  // ceil(sum / n)
 
     uint32_t w[WORDS];
 #pragma unroll
     for (int k = 0; k < WORDS; ++k) w[k] = 0;
-#define BICOS_SET(pos, cond) w[(pos) >> 5] |= (uint32_t)(cond) << ((pos) & 31)
-#pragma unroll
-    for (int t = 0; t < MAXN - 2; ++t) {
-        if (t < n - 2) {
-            const uint32_t x = v[t], y = v[t + 1], z = v[t + 2];
-            const int pos = t < 2 ? 3 * t : 6 + 4 * (t - 2);
-            BICOS_SET(pos + 0, x < y);
-            BICOS_SET(pos + 1, x < z);
-            BICOS_SET(pos + 2, (float)x < av);
-            if (t >= 2) BICOS_SET(pos + 3, v[t - 2] + v[t - 1] < x + y);
-        }
-    }
-#undef BICOS_SET
-    // tail (descriptor_transform.hpp:63-68): a = p[n-2], b = p[n-1]
-    uint32_t x = 0, y = 0, pm2 = 0;
-#pragma unroll
-    for (int t = 0; t < MAXN; ++t) {
-        if (t == n - 2) x = v[t];
-        if (t == n - 1) y = v[t];
-        if (t == n - 4) pm2 = v[t] + v[t + 1];
-    }
-    const uint32_t tail = (uint32_t)(x < y) | ((uint32_t)((float)x < av) << 1) |
-                          ((uint32_t)((float)y < av) << 2) |
+    uint32_t cur = 0;
+    limited_steps<0, MAXN, WORDS>(n, thr, v, cur, w);
+
+    // bits emitted by the loop, the partial word they leave, then the 4 tail bits
+    // (descriptor_transform.hpp:63-68): p[n-2]<p[n-1], p[n-2]<av, p[n-1]<av, ps[n-4]<ps[n-2]
+    const int nl = n >= 4 ? 6 + 4 * (n - 4) : 3 * (n - 2);
+    const int pw = nl >> 5, pm = nl & 31;
+    const uint32_t part = pm ? __builtin_bitreverse32(cur << (32 - pm)) : 0u;
+    // the tail samples sit at n-dependent slots: re-load them (cache hits) rather than
+    // select them out of the register array
+    const uint32_t x = rd((uint32_t)col, rowoff + (uint32_t)(n - 2) * pp);
+    const uint32_t y = rd((uint32_t)col, rowoff + (uint32_t)(n - 1) * pp);
+    const uint32_t pm2 = n >= 4 ? rd((uint32_t)col, rowoff + (uint32_t)(n - 4) * pp) +
+                                      rd((uint32_t)col, rowoff + (uint32_t)(n - 3) * pp)
+                                : 0u;
+    const uint32_t tail = (uint32_t)(x < y) | ((uint32_t)(x < thr) << 1) | ((uint32_t)(y < thr) << 2) |
                           ((uint32_t)(n < 4 || pm2 < x + y) << 3);
-    const int tpos = n >= 4 ? 3 * (n - 2) + (n - 4) : 3 * (n - 2);
-    const int tw = tpos >> 5, toff = tpos & 31;
+    const int tw = nl >> 5, toff = nl & 31;
 #pragma unroll
     for (int k = 0; k < WORDS; ++k) {
+        if (k == pw) w[k] |= part;
         if (k == tw) w[k] |= tail << toff;
         if (k == tw + 1 && toff > 28) w[k] |= tail >> (32 - toff);
     }
@@ -744,7 +845,7 @@ __global__ __launch_bounds__(256) void agree_kernel(AgreeArgs a) {
 
 // agree with the 2n samples loaded once into registers (MAXN >= n), the same arithmetic
 // and output contract as agree_kernel.
-template <typename TIn, typename TPrec, int MAXN>
+template <typename TIn, typename TPrec, int MAXN, bool EXACT>
 __global__ __launch_bounds__(256) void agree_reg_kernel(AgreeArgs a) {
     const int col = blockIdx.x * 256 + threadIdx.x;
     const int row = blockIdx.y;
@@ -757,17 +858,17 @@ __global__ __launch_bounds__(256) void agree_reg_kernel(AgreeArgs a) {
         if (idx1 < 0 || idx1 >= a.cols) {
             d = INVALID_I16;
         } else {
-            const int n = a.n;
+            const int n = EXACT ? MAXN : a.n;
             const size_t pp = a.plane_pitch;
-            const TIn* s0 = (const TIn*)a.stack0 + (size_t)row * a.row_pitch + col;
-            const TIn* s1 = (const TIn*)a.stack1 + (size_t)row * a.row_pitch + idx1;
+            const StackReader<TIn> rd0(a.stack0, a.stack_bytes), rd1(a.stack1, a.stack_bytes);
+            const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
             uint32_t l[MAXN], r[MAXN];
             uint32_t sl = 0, sr = 0;
 #pragma unroll
             for (int t = 0; t < MAXN; ++t)
                 if (t < n) {
-                    l[t] = ld(s0 + t * pp);
-                    r[t] = ld(s1 + t * pp);
+                    l[t] = rd0((uint32_t)col, rowoff + (uint32_t)(t * pp));
+                    r[t] = rd1((uint32_t)idx1, rowoff + (uint32_t)(t * pp));
                     sl += l[t];
                     sr += r[t];
                 }
@@ -800,13 +901,13 @@ __global__ __launch_bounds__(256) void agree_reg_kernel(AgreeArgs a) {
 // agree_subpixel (agree.hpp:95-191). MAXN >= n bounds the per-lane register arrays
 // (static indices only; t >= n iterations are skipped by wave-uniform branches). The
 // quadratic interpolation is float in both precisions (agree.cuh:221-236).
-template <typename TIn, typename TPrec, int MAXN>
+template <typename TIn, typename TPrec, int MAXN, bool EXACT>
 __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
     const int col = blockIdx.x * 256 + threadIdx.x;
     const int row = blockIdx.y;
     if (col >= a.cols) return;
     const size_t o = (size_t)row * a.cols + col;
-    const int n = a.n;
+    const int n = EXACT ? MAXN : a.n;
     const size_t pp = a.plane_pitch;
     const int d = a.raw[(size_t)row * a.raw_pitch + col];
     const TPrec minvar = (TPrec)a.minvar;
@@ -820,6 +921,8 @@ __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
             corr = nxcorr_dev<TIn, TPrec>(s0, s1, pp, n, a.has_minvar, minvar);
             if (!(corr < (TPrec)a.threshold)) out = (float)d;
         } else {
+            const StackReader<TIn> rd0(a.stack0, a.stack_bytes), rd1(a.stack1, a.stack_bytes);
+            const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
             // left: mean, centred samples and variance are the same for every x
             TPrec D0[MAXN];
             float A[MAXN], B[MAXN], C[MAXN];
@@ -827,12 +930,13 @@ __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
 #pragma unroll
             for (int t = 0; t < MAXN; ++t)
                 if (t < n) {
-                    const uint32_t l = ld(s0 + t * pp);
+                    const uint32_t po = rowoff + (uint32_t)(t * pp);
+                    const uint32_t l = rd0((uint32_t)col, po);
                     D0[t] = (TPrec)l;
                     s += l;
-                    const int y0 = (int)ld(s1 - 1 + t * pp);
-                    const int y1 = (int)ld(s1 + t * pp);
-                    const int y2 = (int)ld(s1 + 1 + t * pp);
+                    const int y0 = (int)rd1((uint32_t)(col1 - 1), po);
+                    const int y1 = (int)rd1((uint32_t)col1, po);
+                    const int y2 = (int)rd1((uint32_t)(col1 + 1), po);
                     // 0.5f * ( y0 - 2.0f * y1 + y2) ; 0.5f * (-y0 + y2) ; y1
                     A[t] = 0.5f * (((float)y0 - 2.0f * (float)y1) + (float)y2);
                     B[t] = 0.5f * (float)(-y0 + y2);
@@ -895,7 +999,10 @@ __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
 
 template <typename TIn, int WORDS, int MAXN>
 hipError_t launch_tl(const TransformArgs& a, dim3 grid, hipStream_t st) {
-    hipLaunchKernelGGL((transform_limited_kernel<TIn, WORDS, MAXN>), grid, dim3(256), 0, st, a);
+    if (a.n == MAXN)
+        hipLaunchKernelGGL((transform_limited_kernel<TIn, WORDS, MAXN, true>), grid, dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((transform_limited_kernel<TIn, WORDS, MAXN, false>), grid, dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
@@ -981,7 +1088,10 @@ hipError_t launch_search_w(const SearchArgs& a, bool nodupes, const SearchGeomet
 template <typename TIn, typename TPrec, int MAXN>
 hipError_t launch_subpixel_m(const AgreeArgs& a, hipStream_t st) {
     dim3 grid((a.cols + 255) / 256, a.rows);
-    hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN>), grid, dim3(256), 0, st, a);
+    if (a.n == MAXN)
+        hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN, true>), grid, dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN, false>), grid, dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
@@ -1002,7 +1112,10 @@ hipError_t launch_subpixel_t(const AgreeArgs& a, hipStream_t st) {
 template <typename TIn, typename TPrec, int MAXN>
 hipError_t launch_agree_m(const AgreeArgs& a, hipStream_t st) {
     dim3 grid((a.cols + 255) / 256, a.rows);
-    hipLaunchKernelGGL((agree_reg_kernel<TIn, TPrec, MAXN>), grid, dim3(256), 0, st, a);
+    if (a.n == MAXN)
+        hipLaunchKernelGGL((agree_reg_kernel<TIn, TPrec, MAXN, true>), grid, dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((agree_reg_kernel<TIn, TPrec, MAXN, false>), grid, dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
@@ -1026,9 +1139,11 @@ hipError_t launch_agree_t(const AgreeArgs& a, hipStream_t st) {
 
 // ------------------------------------------------------------ public launchers
 
-hipError_t launch_transform(const TransformArgs& a, int depth, int mode, int words, hipStream_t st) {
+hipError_t launch_transform(TransformArgs a, int depth, int mode, int words, hipStream_t st) {
     if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
     if (mode == 1 && a.n > 16) return hipErrorInvalidValue;
+    if (a.n < 2) return hipErrorInvalidValue;
+    a.magic = (uint32_t)((0x100000000ull + (uint64_t)a.n - 1) / (uint64_t)a.n);
     return depth == 1 ? launch_transform_t<uint8_t>(a, mode, words, st)
                       : launch_transform_t<uint16_t>(a, mode, words, st);
 }

@@ -17,6 +17,8 @@ struct TransformArgs {
     size_t row_pitch;       // elements
     size_t plane_pitch;     // elements
     size_t desc_pitch;      // uint32 words per descriptor row
+    uint32_t magic;         // ceil(2^32 / n): exact sum / n by umulhi (set by launch_transform)
+    uint32_t stack_bytes;   // bytes addressable from each stack base (< 4 GiB)
 };
 
 struct SearchArgs {
@@ -64,9 +66,10 @@ struct AgreeArgs {
     void* out;              // dense [rows][cols]
     int out_f32;            // agree: 1 -> float32 output, 0 -> int16 in place semantics
     void* corrmap;          // dense [rows][cols] float (double for DOUBLE) or nullptr
+    uint32_t stack_bytes;   // bytes addressable from each stack base (< 4 GiB)
 };
 
-hipError_t launch_transform(const TransformArgs& a, int depth, int mode, int words, hipStream_t st);
+hipError_t launch_transform(TransformArgs a, int depth, int mode, int words, hipStream_t st);
 SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes, int variant = 16,
                                int R = 0, int waves = 0, int split = 0);
 hipError_t launch_search(SearchArgs a, const SearchGeometry& g, int words, bool nodupes,
