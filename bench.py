@@ -29,10 +29,15 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# MI355X (gfx950) peaks, /opt/skills/guides/MI355X_MICROARCH.md "Chip-level parameters":
-# 256 CUs x 4 SIMD-32 x 2.4 GHz -> 128 int32 lane-ops/clk/CU = 78.6 T lane-op/s
-VALU_PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12
+# MI355X (gfx950) peaks. HBM: /opt/skills/guides/MI355X_MICROARCH.md "Chip-level
+# parameters" (8 TB/s). VALU: the guide gives no integer rates, so they were measured on
+# the box (tools/valu_peak.hip -> profiles/valu_rates_r01.json): v_xor/v_and/v_add/v_mov
+# issue at full rate, ~72 T lane-op/s (128 lanes/clk/CU at the held clock); v_bcnt,
+# v_min/med3, v_lshl_or, v_perm, v_pk_*_u16 at half rate, ~38.5 T lane-op/s.
 HBM_PEAK_GBS = 8000.0
+VALU_FULL_TOPS = 72.0
+VALU_HALF_TOPS = 38.5
+VALU_NOMINAL_TOPS = 256 * 128 * 2.4e9 / 1e12   # 78.6: every op at full rate, 2.4 GHz
 
 CONFIGS = {
     # BASELINE.json configs; "cfg2" is the one the headline metric is quoted on
@@ -51,14 +56,47 @@ CONFIGS = {
 }
 
 
+def search_pairs(rows: int, W: int, cfg: dict) -> float:
+    """Hamming pairs the search evaluates per match: every (col0, col1) of every row,
+    once per direction (twice with Consistency)."""
+    return float(rows) * W * W * (2 if cfg.get("variant", 0) == 1 else 1)
+
+
+def search_pair_peak(words: int, cfg: dict) -> float:
+    """Issue-rate bound in pairs/s of the packed search loop's per-pair instruction mix at
+    the measured VALU rates: `words` v_xor (full rate) + `words` v_bcnt (half rate) + half
+    a v_perm and half a v_pk_min_u16 (2 col0 share one packed key register) + with
+    duplicate detection another half v_xor (full) and half v_pk_min_u16 (half rate)."""
+    dupes = cfg.get("variant", 0) == 0 or cfg.get("no_dupes", False)
+    full = words + (0.5 if dupes else 0.0)
+    half = words + 1.0 + (0.5 if dupes else 0.0)
+    per_pair_s = full / (VALU_FULL_TOPS * 1e12) + half / (VALU_HALF_TOPS * 1e12)
+    return 1.0 / per_pair_s
+
+
 def search_ops(rows: int, W: int, words: int, cfg: dict) -> float:
-    """Algorithmic INT32 lane-ops of the search kernel launches of one match:
-    per (col0, col1) pair: `words` xor + `words` bcnt + key pack + min (+ med3 with
-    NoDuplicates)  = 2w+3 (NoDuplicates) / 2w+2 per direction (Consistency)."""
-    if cfg.get("variant", 0) == 1:
-        per = 2 * words + (3 if cfg.get("no_dupes") else 2)
-        return 2.0 * rows * W * W * per
-    return float(rows) * W * W * (2 * words + 3)
+    """Reference-algorithm INT32 lane-ops (32-bit keys): per pair `words` xor + `words`
+    bcnt + key pack + min (+ med3 with NoDuplicates) = 2w+3 (2w+2 without)."""
+    dupes = cfg.get("variant", 0) == 0 or cfg.get("no_dupes", False)
+    return search_pairs(rows, W, cfg) * (2 * words + (3 if dupes else 2))
+
+
+def load_traffic(kernel_prefix: str, rows: int, W: int):
+    """Per-launch HBM bytes of the search kernel from the committed PMC summary (the
+    latest profiles/pmc_r*.json whose grid matches), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        for key, c in d.get("kernels", {}).items():
+            if key.startswith(kernel_prefix) and "hbm_read_bytes" in c and "hbm_write_bytes" in c \
+                    and c.get("rows") in (None, rows):
+                return {"bytes": c["hbm_read_bytes"] + c["hbm_write_bytes"],
+                        "source": os.path.relpath(f, ROOT) + " :: " + key}
+    return None
 
 
 def main():
@@ -73,6 +111,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target wall time of the CPU baseline sample")
     ap.add_argument("--kernel-reps", type=int, default=10)
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (production); gloo = rehearsal of the N>1 "
+                         "path with several ranks sharing one GPU (not a measurement)")
     args = ap.parse_args()
 
     import numpy as np
@@ -88,10 +129,17 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d (launch N>1 with torchrun)" % (args.gpus, world))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    ndev = torch.cuda.device_count()
+    if args.backend == "nccl" and local >= ndev:
+        raise SystemExit("rank %d has no GPU (%d visible)" % (local, ndev))
+    local_dev = local % ndev
+    torch.cuda.set_device(local_dev)
+    dev = torch.device("cuda", local_dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     C = CONFIGS[args.config]
     n, H, W = C["n"], C["H"], C["W"]
@@ -108,7 +156,7 @@ def main():
     s0 = torch.from_numpy(L).to(dev)
     s1 = torch.from_numpy(R).to(dev)
     del L, R
-    eng = device.Engine(local)
+    eng = device.Engine(local_dev)
     has_corr = mcfg.nxcorr_threshold is not None
     out = torch.empty((rows, W), dtype=torch.float32 if has_corr else torch.int16, device=dev)
     corr = torch.empty((rows, W), dtype=torch.float32, device=dev) if has_corr else None
@@ -118,7 +166,8 @@ def main():
         hb = band_height(H, world)
         # one packed buffer -> one RCCL gather per step (disparity + corrmap bands)
         planes = 2 if has_corr else 1
-        send = torch.zeros((planes, hb, W), dtype=torch.float32, device=dev)
+        gdev = dev if args.backend == "nccl" else torch.device("cpu")
+        send = torch.zeros((planes, hb, W), dtype=torch.float32, device=gdev)
         recv = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
 
     def step():
@@ -142,7 +191,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -173,24 +223,38 @@ def main():
     t_search = ev[0].elapsed_time(ev[1]) / args.kernel_reps * 1e-3
     t_tf = ev[1].elapsed_time(ev[2]) / args.kernel_reps * 1e-3
     t_agree = ev[3].elapsed_time(ev[4]) / args.kernel_reps * 1e-3
-    ops = search_ops(rows, W, words, C["cfg"])
-    achieved = ops / t_search / 1e12
+    pairs = search_pairs(rows, W, C["cfg"])
+    achieved = pairs / t_search / 1e9
+    peak = search_pair_peak(words, C["cfg"]) / 1e9
     # HBM stages, algorithmic bytes: transform reads n B/px and writes 4w B/px (one stack);
     # agree reads the int16 raw disparity + 2n B per valid px, writes 8 B/px (disp + corr)
     tf_bytes = rows * W * (n + 4 * words)
     valid = float((raw != -32768).float().mean().item())
     ag_bytes = rows * W * (2 + 8) + rows * W * valid * 2 * n
+    # algorithmic bytes of one search launch: both descriptor bands + the int16 output
+    search_bytes = rows * W * (2 * 4 * words + 2)
+    traffic = load_traffic("search16_kernel", rows, W) if args.config == "cfg2" and rows == H else None
 
     roof = {
-        "kernel": "search_kernel<%d words>" % words,
+        "kernel": "search16_kernel<%d words> (Hamming argmin, packed 16-bit keys)" % words,
         "bound": "valu",
-        "achieved": round(achieved, 2),
-        "peak": round(VALU_PEAK_TOPS, 2),
-        "unit": "Tops/s (int32 lane-ops)",
-        "frac": round(achieved / VALU_PEAK_TOPS, 4),
-        "traffic": None,
-        "ops_per_launch": ops,
+        "achieved": round(achieved, 1),
+        "peak": round(peak, 1),
+        "unit": "Gpairs/s",
+        "frac": round(achieved / peak, 4),
+        "traffic": None if traffic is None else traffic["bytes"],
+        "traffic_source": None if traffic is None else traffic["source"],
+        "algorithmic_bytes": search_bytes,
+        "pairs_per_launch": pairs,
         "ms_per_launch": round(t_search * 1e3, 4),
+        "peak_model": "issue bound of the per-pair VALU mix at measured rates "
+                      "(full %.1f / half %.1f T lane-op/s); see DESIGN.md s5" %
+                      (VALU_FULL_TOPS, VALU_HALF_TOPS),
+        "lane_ops_view": {
+            "achieved_Tops": round(search_ops(rows, W, words, C["cfg"]) / t_search / 1e12, 2),
+            "nominal_peak_Tops": round(VALU_NOMINAL_TOPS, 1),
+            "ops_model": "reference algorithm, 32-bit keys: 2w+3 lane-ops per pair",
+        },
         "hbm": {
             "transform_GBps": round(tf_bytes / t_tf / 1e9, 1),
             "transform_frac": round(tf_bytes / t_tf / 1e9 / HBM_PEAK_GBS, 4),

@@ -43,21 +43,24 @@ def gather_bands(band: torch.Tensor, H: int, group=None, dst: int = 0) -> Option
     if band.shape[0] != e - b:
         raise ValueError("band has %d rows, expected %d" % (band.shape[0], e - b))
     if band.shape[0] != hb:
-        pad = torch.empty((hb,) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
+        pad = torch.zeros((hb,) + tuple(band.shape[1:]), dtype=band.dtype, device=band.device)
         pad[: band.shape[0]] = band
         band = pad
     else:
         band = band.contiguous()
+    # collectives do not all take int16 (neither gloo nor RCCL): move raw bytes
+    dtype = band.dtype
+    raw = band.reshape(hb, -1).view(torch.uint8)
     parts: Optional[List[torch.Tensor]] = None
     if rank == dst:
-        parts = [torch.empty_like(band) for _ in range(world)]
-    dist.gather(band, parts, dst=dst, group=group)
+        parts = [torch.empty_like(raw) for _ in range(world)]
+    dist.gather(raw, parts, dst=dst, group=group)
     if rank != dst:
         return None
     rows = []
     for r in range(world):
         rb, re = band_rows(H, world, r)
-        rows.append(parts[r][: re - rb])
+        rows.append(parts[r][: re - rb].view(dtype).reshape((re - rb,) + tuple(band.shape[1:])))
     return torch.cat(rows, dim=0)
 
 

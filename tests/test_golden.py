@@ -1,0 +1,57 @@
+"""Committed golden vectors (tests/golden/golden.npz, oracle-generated; see
+tests/golden/make_golden.py) against the oracle (CPU) and the HIP path (GPU)."""
+import os
+
+import numpy as np
+import pytest
+
+from tests.golden.make_golden import CASES, CONFIGS, inputs, sha
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden.npz")
+
+
+@pytest.fixture(scope="module")
+def golden():
+    return np.load(GOLDEN, allow_pickle=False)
+
+
+def _same(a, b):
+    return a.dtype == b.dtype and a.shape == b.shape and np.array_equal(a.view(np.uint8),
+                                                                        b.view(np.uint8))
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_inputs_unchanged(golden, case):
+    name, n, H, W, dt, mode, gen = case
+    L, R = inputs(n, H, W, dt, gen)
+    assert str(golden[name + "/inputs_sha256"]) == sha(L) + sha(R)
+
+
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_oracle_reproduces_golden(oracle, golden, case):
+    name, n, H, W, dt, mode, gen = case
+    L, R = inputs(n, H, W, dt, gen)
+    for cname, cfg in CONFIGS:
+        d, corr = oracle.match(L, R, oracle.OracleConfig(mode=mode, **cfg))
+        assert _same(d, golden["%s/%s/disparity" % (name, cname)]), (name, cname)
+        if corr is not None:
+            assert _same(corr, golden["%s/%s/corrmap" % (name, cname)]), (name, cname)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", CASES, ids=[c[0] for c in CASES])
+def test_gpu_reproduces_golden(gpu, golden, case):
+    import torch
+    from libbicos_amd.device import MatchConfig
+    name, n, H, W, dt, mode, gen = case
+    L, R = inputs(n, H, W, dt, gen)
+
+    def dev(a):
+        a = np.ascontiguousarray(a)
+        return torch.from_numpy(a.view(np.int16) if a.dtype == np.uint16 else a).cuda()
+
+    for cname, cfg in CONFIGS:
+        d, corr = gpu.match(dev(L), dev(R), MatchConfig(mode=mode, **cfg))
+        assert _same(d.cpu().numpy(), golden["%s/%s/disparity" % (name, cname)]), (name, cname)
+        if corr is not None:
+            assert _same(corr.cpu().numpy(), golden["%s/%s/corrmap" % (name, cname)]), (name, cname)

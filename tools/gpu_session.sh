@@ -28,6 +28,7 @@ for step in "$@"; do
         sweep1) run sweep1 600 python tools/search_sweep.py --config cfg1 --variants 32:1:4,32:2:4,16:2:4,16:4:4,16:2:2,16:2:1 ;;
         sweep8) run sweep8 600 python tools/search_sweep.py --rows 192 --variants 16:2:8:4,17:2:8:4,16:4:8:4,17:4:8:4,16:2:8:2,17:2:8:2 ;;
         sweep5) run sweep5 600 python tools/search_sweep.py --config cfg5 --rows 270 --variants 0:0:0:0,16:2:8:1,16:2:8:2,16:2:8:4 ;;
+        rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --steps 5 --warmup 1 --no-cpu-baseline ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
         pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 2 ;;
         pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 2 ;;
