@@ -7,7 +7,9 @@ A step = one full BICOS::match of the configured synthetic stereo frame
 (transform x2 -> Hamming search -> NXC agree [-> subpixel]) with the planar
 stacks already resident in HBM. With N > 1 the frame is split into N row bands
 (one per GPU, strong scaling) and the disparity + correlation bands are gathered
-to rank 0 with ONE RCCL gather per step, inside the timed region.
+to rank 0 with ONE RCCL gather per step, inside the timed region; the gather of
+step k overlaps the kernels of step k+1 (double-buffered), and every gather has
+completed before the closing barrier.
 
 Extra keys on the JSON line:
   roofline      the dominant kernel (the Hamming search), timed live with HIP
@@ -164,28 +166,52 @@ def main():
     gather = world > 1 and args.scaling == "strong"
     if gather:
         hb = band_height(H, world)
-        # one packed buffer -> one RCCL gather per step (disparity + corrmap bands)
+        # one packed [disparity | corrmap] band buffer -> ONE RCCL gather per step. The
+        # match writes straight into it (no copies), and two buffers alternate so step
+        # k's gather (RCCL stream) overlaps step k+1's kernels (compute stream).
         planes = 2 if has_corr else 1
         gdev = dev if args.backend == "nccl" else torch.device("cpu")
-        send = torch.zeros((planes, hb, W), dtype=torch.float32, device=gdev)
-        recv = [torch.empty_like(send) for _ in range(world)] if rank == 0 else None
+        sends = [torch.zeros((planes, hb, W), dtype=torch.float32, device=gdev) for _ in range(2)]
+        recvs = [[torch.empty_like(sends[0]) for _ in range(world)] if rank == 0 else None
+                 for _ in range(2)]
+        pending = [None, None]
+    state = {"k": 0}
 
     def step():
-        eng.match(s0, s1, mcfg, out=out, corrmap=corr)
-        if gather:
-            send[0, :rows].copy_(out if has_corr else out.float())
+        if not gather:
+            eng.match(s0, s1, mcfg, out=out, corrmap=corr)
+            return
+        i = state["k"] % 2
+        state["k"] += 1
+        if pending[i] is not None:
+            pending[i].wait()  # the compute stream waits for the gather that last read sends[i]
+        buf = sends[i]
+        if has_corr and args.backend == "nccl":
+            eng.match(s0, s1, mcfg, out=buf[0, :rows], corrmap=buf[1, :rows])
+        else:
+            eng.match(s0, s1, mcfg, out=out, corrmap=corr)
+            buf[0, :rows].copy_(out if has_corr else out.float())
             if has_corr:
-                send[1, :rows].copy_(corr)
-            dist.gather(send, recv, dst=0)
+                buf[1, :rows].copy_(corr)
+        pending[i] = dist.gather(buf, recvs[i], dst=0, async_op=True)
+
+    def drain():
+        if gather:
+            for i in range(2):
+                if pending[i] is not None:
+                    pending[i].wait()
+                    pending[i] = None
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()

@@ -104,7 +104,7 @@ void bicos_engine_destroy(bicos_engine* e);
  *                  as one inline-asm block, 32 = 32-bit keys
  *   col0_per_lane  left pixels held in registers per lane (16: 2|4; 32: 1|2|4)
  *   waves          waves per workgroup (1..8)
- *   split          waves that share one col0 group and split its col1 scan (1|2|4, variant 16)
+ *   split          waves that share one col0 group and split its col1 scan (1|2|4|8, variant 16)
  * Results are identical for every setting; only speed changes. */
 int bicos_engine_tune(bicos_engine* e, int variant, int col0_per_lane, int waves, int split);
 

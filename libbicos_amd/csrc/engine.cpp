@@ -79,7 +79,7 @@ bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, in
     const int max_lds = e ? e->max_lds : 64 * 1024;
     if (!e) return bicos_hip::search_geometry(rows, cols, words, max_lds);
     return bicos_hip::search_geometry(rows, cols, words, max_lds, e->tune_variant, e->tune_R,
-                                      e->tune_waves, e->tune_split);
+                                      e->tune_waves, e->tune_split, e->cus);
 }
 
 static int required_bits(int n, int mode) { return mode ? n * n - 2 * n + 3 : 4 * n - 7; }
@@ -238,6 +238,10 @@ int bicos_engine_create(int device, bicos_engine** out) {
         // keep the per-workgroup right-row stage <= 64 KiB so >= 2 workgroups fit per CU
         e->max_lds = lds < 64 * 1024 ? lds : 64 * 1024;
     }
+    int cus = 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
+        cus > 0)
+        e->cus = cus;
     rc = check_hip(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking), "hipStreamCreate");
     (void)hipSetDevice(cur);
     if (rc) {
@@ -263,15 +267,16 @@ void bicos_engine_destroy(bicos_engine* e) {
 
 int bicos_engine_tune(bicos_engine* e, int variant, int col0_per_lane, int waves, int split) {
     if (!e) return fail(BICOS_E_ARG, "null engine");
-    if (variant != 0 && variant != 16 && variant != 17 && variant != 32)
-        return fail(BICOS_E_ARG, "variant 0|16|17|32");
-    const int v = variant == 17 ? 16 : (variant ? variant : 16);
+    if (variant != 0 && variant != 16 && variant != 17 && variant != 18 && variant != 32)
+        return fail(BICOS_E_ARG, "variant 0|16|17|18|32");
+    const int v = (variant == 17 || variant == 18) ? 16 : (variant ? variant : 16);
     if (col0_per_lane != 0 && !(v == 16 ? (col0_per_lane == 2 || col0_per_lane == 4)
                                         : (col0_per_lane == 1 || col0_per_lane == 2 ||
                                            col0_per_lane == 4)))
         return fail(BICOS_E_ARG, "col0_per_lane: 2|4 (variant 16), 1|2|4 (variant 32)");
     if (waves < 0 || waves > 8) return fail(BICOS_E_ARG, "waves 1..8");
-    if (split != 0 && split != 1 && split != 2 && split != 4) return fail(BICOS_E_ARG, "split 1|2|4");
+    if (split != 0 && split != 1 && split != 2 && split != 4 && split != 8)
+        return fail(BICOS_E_ARG, "split 1|2|4|8");
     if (split > 1 && (v != 16 || (waves ? waves : 8) % split))
         return fail(BICOS_E_ARG, "split needs variant 16 and waves divisible by split");
     e->tune_variant = variant;

@@ -16,6 +16,7 @@
 struct bicos_engine {
     int device = 0;
     int max_lds = 64 * 1024;
+    int cus = 256;                     // compute units (workgroup geometry)
     // search kernel tuning (0 = automatic): see bicos_engine_tune
     int tune_variant = 0, tune_R = 0, tune_waves = 0, tune_split = 0;
     hipStream_t own_stream = nullptr;  // used by the host-buffer APIs

@@ -591,6 +591,25 @@ __device__ __forceinline__ uint32_t ham_seeded(const uint32_t (&a)[WORDS], const
     return c;
 }
 
+// Both col0 chains interleaved word by word; one instruction-free asm per word keeps the
+// two accumulators opaque (no v_add3 re-association) and the first v_bcnt takes the
+// col1 seed straight from its SGPR.
+template <int WORDS>
+__device__ __forceinline__ void ham_pair(const uint32_t (&a)[WORDS], const uint32_t (&b)[WORDS],
+                                         const uint32_t (&d)[WORDS], uint32_t seed, uint32_t& r0,
+                                         uint32_t& r1) {
+    uint32_t c0 = __builtin_popcount(a[0] ^ d[0]) + seed;
+    uint32_t c1 = __builtin_popcount(b[0] ^ d[0]) + seed;
+#pragma unroll
+    for (int k = 1; k < WORDS; ++k) {
+        asm("" : "+v"(c0), "+v"(c1));
+        c0 = __builtin_popcount(a[k] ^ d[k]) + c0;
+        c1 = __builtin_popcount(b[k] ^ d[k]) + c1;
+    }
+    r0 = c0;
+    r1 = c1;
+}
+
 template <int WORDS, bool NODUPES, int RP, int STEP>
 __device__ __forceinline__ void search16_step(const uint32_t* s, uint32_t seed,
                                               const uint32_t (&d0)[2 * RP][WORDS],
@@ -601,6 +620,12 @@ __device__ __forceinline__ void search16_step(const uint32_t* s, uint32_t seed,
     for (int p = 0; p < RP; ++p) {
         if (STEP == 1) {
             pair_step<WORDS, NODUPES>(d1, d0[2 * p], d0[2 * p + 1], seed, lo[p], hi[p]);
+        } else if (STEP == 2) {
+            uint32_t r0, r1;
+            ham_pair<WORDS>(d0[2 * p], d0[2 * p + 1], d1, seed, r0, r1);
+            const uint32_t key = __builtin_amdgcn_perm(r1, r0, 0x04050001u);
+            lo[p] = pk_min_u16(lo[p], key);
+            if (NODUPES) hi[p] = pk_min_u16(hi[p], key ^ 0x00FF00FFu);
         } else {
             const uint32_t r0 = ham_seeded<WORDS>(d0[2 * p], d1, seed);
             const uint32_t r1 = ham_seeded<WORDS>(d0[2 * p + 1], d1, seed);
@@ -1071,6 +1096,13 @@ hipError_t launch_search_n(const SearchArgs& a, const SearchGeometry& g, hipStre
         }
         return hipErrorInvalidValue;
     }
+    if (g.variant == 18) {
+        switch (g.R) {
+            case 2: return launch_search16_r<WORDS, NODUPES, 1, 2>(a, g.waves, st);
+            case 4: return launch_search16_r<WORDS, NODUPES, 2, 2>(a, g.waves, st);
+        }
+        return hipErrorInvalidValue;
+    }
     switch (g.R) {
         case 1: return launch_search_r<WORDS, NODUPES, 1>(a, g.waves, st);
         case 2: return launch_search_r<WORDS, NODUPES, 2>(a, g.waves, st);
@@ -1149,9 +1181,9 @@ hipError_t launch_transform(TransformArgs a, int depth, int mode, int words, hip
 }
 
 SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes, int variant,
-                               int R, int waves, int split) {
+                               int R, int waves, int split, int cus) {
     SearchGeometry g;
-    g.variant = (variant == 32 || variant == 17) ? variant : 16;
+    g.variant = (variant == 32 || variant == 17 || variant == 18) ? variant : 16;
     // col1 chunk staged per LDS fill: the whole row when it fits
     const int max_chunk = max_lds_bytes / (words * 4);
     g.chunk = cols < max_chunk ? cols : max_chunk;
@@ -1165,14 +1197,26 @@ SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes,
     } else if (split) {
         g.split = split;
     } else {
-        // split the col1 scan across waves until ~32 waves per CU are in flight
+        // Split the col1 scan across waves so the grid fills whole "rounds" of resident
+        // waves (CUs x 32): a round that is only partly filled idles the rest of the chip
+        // (192-row bands, 8 GPUs: 1.5 rounds at split 4 vs 3.0 at split 8).
         const long base = (long)rows * ((cols + 64L * g.R - 1) / (64L * g.R));
         const int tiles256 = (cols + 255) / 256;
+        const double slots = (double)(cus > 0 ? cus : 256) * 32.0;
+        double best = -1.0;
         g.split = 1;
-        // measured best: cfg2 full frame split 2, 192-row band split 4, 270x3840 split 4
-        while (g.split < 4 && base * g.split < 256L * 128 && tiles256 >= 2 * g.split &&
-               g.waves % (2 * g.split) == 0)
-            g.split *= 2;
+        for (int sp = 1; sp <= 8; sp *= 2) {
+            if (sp > 1 && (tiles256 < sp || g.waves % sp)) break;
+            const double rounds = (double)(base * sp) / slots;
+            const double fill = rounds / __builtin_ceil(rounds);
+            // prefer a full last round, then up to 3 rounds in flight, then a smaller split
+            const double score = fill + 0.1 * (rounds < 3.0 ? rounds : 3.0) / 3.0 -
+                                 0.005 * (double)__builtin_ctz(sp);
+            if (score > best + 1e-9) {
+                best = score;
+                g.split = sp;
+            }
+        }
     }
     const long per_wg = 64L * (g.waves / g.split) * g.R;
     g.tiles_per_row = (int)((cols + per_wg - 1) / per_wg);

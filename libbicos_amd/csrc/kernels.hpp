@@ -40,7 +40,7 @@ struct SearchGeometry {
     int R;                  // col0 per lane
     int tiles_per_row;
     int variant;            // 16: packed 16-bit keys (default), 32: 32-bit keys
-    int split;              // packed variant: col1 split across waves of a workgroup (1, 2, 4)
+    int split;              // packed variant: col1 split across waves of a workgroup (1, 2, 4, 8)
 };
 
 struct ConsistencyArgs {
@@ -71,7 +71,7 @@ struct AgreeArgs {
 
 hipError_t launch_transform(TransformArgs a, int depth, int mode, int words, hipStream_t st);
 SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes, int variant = 16,
-                               int R = 0, int waves = 0, int split = 0);
+                               int R = 0, int waves = 0, int split = 0, int cus = 256);
 hipError_t launch_search(SearchArgs a, const SearchGeometry& g, int words, bool nodupes,
                          hipStream_t st);
 hipError_t launch_consistency(const ConsistencyArgs& a, hipStream_t st);
