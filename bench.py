@@ -241,9 +241,16 @@ def main():
     for _ in range(args.kernel_reps):
         eng.transform(s0, mcfg.mode, words, out=d0)
     ev[2].record(st)
+    # the agree stage this config runs: NXC (agree_reg_kernel) or NXC + subpixel refine
+    mc = C["cfg"]
+    thr = mc.get("nxcorr_threshold")
+    mv = mc.get("min_variance")
+    mv = None if mv is None or mv < 0 else mv * n
+    stage = "subpixel" if mc.get("subpixel_step") else "nxcorr"
     ev[3].record(st)
     for _ in range(args.kernel_reps):
-        eng.agree(raw, s0, s1, 0.96)
+        eng.agree(raw, s0, s1, 0.96 if thr is None else thr, minvar_scaled=mv,
+                  step=mc.get("subpixel_step"))
     ev[4].record(st)
     torch.cuda.synchronize(dev)
     t_search = ev[0].elapsed_time(ev[1]) / args.kernel_reps * 1e-3
@@ -288,6 +295,7 @@ def main():
             "agree_GBps": round(ag_bytes / t_agree / 1e9, 1),
             "agree_frac": round(ag_bytes / t_agree / 1e9 / HBM_PEAK_GBS, 4),
             "agree_ms": round(t_agree * 1e3, 4),
+            "agree_stage": stage,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
         },

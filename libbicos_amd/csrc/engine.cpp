@@ -82,6 +82,18 @@ bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, in
                                       e->tune_waves, e->tune_split, e->cus);
 }
 
+// Number of x the reference's subpixel loop visits: for (float x = -1.f; x <= 1.f; x += step)
+// (agree.hpp:122 / agree.cuh:213), accumulated in float exactly as there. 0 when the loop
+// would exceed MAX_SUBPIXEL_STEPS (or never end: x + step == x), which the reference would
+// run for hours on a CPU and which on a GPU is a hung device; such steps are rejected.
+constexpr int MAX_SUBPIXEL_STEPS = 65536;
+int subpixel_steps(float step) {
+    int count = 0;
+    for (float x = -1.f; x <= 1.f; x += step)
+        if (++count > MAX_SUBPIXEL_STEPS) return 0;
+    return count;
+}
+
 static int required_bits(int n, int mode) { return mode ? n * n - 2 * n + 3 : 4 * n - 7; }
 
 // Bytes the kernels may address from a stack base; the kernels use 32-bit buffer offsets.
@@ -119,6 +131,9 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     const bool has_step = has_nxcorr && cfg.subpixel_step >= 0;
     if (has_step && !(cfg.subpixel_step > 0 && std::isfinite(cfg.subpixel_step)))
         return fail(BICOS_E_ARG, "subpixel_step must be a positive finite number");
+    const int nsteps = has_step ? subpixel_steps(cfg.subpixel_step) : 0;
+    if (has_step && !nsteps)
+        return fail(BICOS_E_ARG, "subpixel_step too small (more than 65536 interpolation steps)");
     if (rows == 0 || cols == 0) return BICOS_OK;
     if (!s0 || !s1 || !disp) return fail(BICOS_E_ARG, "null buffer");
     if (row_pitch < (size_t)cols || plane_pitch < (size_t)rows * row_pitch)
@@ -184,6 +199,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     aa.plane_pitch = plane_pitch;
     aa.threshold = threshold;
     aa.step = has_step ? cfg.subpixel_step : 0.f;
+    aa.nsteps = nsteps;
     aa.has_minvar = cfg.min_variance >= 0;
     aa.minvar = aa.has_minvar ? cfg.min_variance * (float)n : 0.f;  // cpu.cpp:127
     aa.out = disp;
@@ -376,6 +392,9 @@ static int agree_common(bool sub, const int16_t* raw, const void* stack0, const 
     if (depth != 1 && depth != 2) return fail(BICOS_E_ARG, "bad input depth");
     if (sub && !(step > 0 && std::isfinite(step)))
         return fail(BICOS_E_ARG, "subpixel_step must be a positive finite number");
+    const int nsteps = sub ? subpixel_steps(step) : 0;
+    if (sub && !nsteps)
+        return fail(BICOS_E_ARG, "subpixel_step too small (more than 65536 interpolation steps)");
     bicos_hip::AgreeArgs aa{};
     aa.raw = raw;
     aa.raw_pitch = (size_t)cols;
@@ -388,6 +407,7 @@ static int agree_common(bool sub, const int16_t* raw, const void* stack0, const 
     aa.plane_pitch = plane_pitch;
     aa.threshold = threshold;
     aa.step = step;
+    aa.nsteps = nsteps;
     aa.has_minvar = has_minvar;
     aa.minvar = minvar_scaled;
     aa.out = out;

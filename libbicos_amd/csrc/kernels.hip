@@ -923,16 +923,51 @@ __global__ __launch_bounds__(256) void agree_reg_kernel(AgreeArgs a) {
     if (a.corrmap) ((TPrec*)a.corrmap)[o] = corr;
 }
 
+// (TIn)roundevenf(A x^2 + B x + C) as a float (agree.cuh:221-236 / agree.hpp:140-150):
+// adding 1.5*2^23 rounds v to the nearest even integer k (|v| < 2^22 for 8/16-bit data)
+// and leaves k's two's-complement low bits in the mantissa, so the low byte/short of the
+// sum's bits IS (TIn)(int)k, the reference's wrap through int32. It goes back to float
+// exactly as (2^23 | low bits) - 2^23; the sum's top byte is always 0x4B, so that is one
+// full-rate AND with 0x4B0000FF (0x4B00FFFF) and a subtract, instead of the quarter-rate
+// v_cvt_f32_ubyte0 (tools/valu_peak.hip, op 19).
+constexpr float RND_MAGIC = 0x1.8p23f;
+
+// (float)k for |k| < 2^22, exactly: full-rate integer add + float subtract
+__device__ __forceinline__ float small_int_to_float(int k) {
+    uint32_t b = 0x4B400000u + (uint32_t)k;
+    asm("" : "+v"(b));  // keep LLVM from folding this back into v_cvt_f32_i32
+    return __uint_as_float(b) - RND_MAGIC;
+}
+template <typename TIn>
+constexpr uint32_t wrap_mask() { return sizeof(TIn) == 1 ? 0x4B0000FFu : 0x4B00FFFFu; }
+
+template <typename TIn>
+__device__ __forceinline__ float interp_wrapped(float A, float B, float C, float x) {
+    const float ax = A * x;
+    const float v = (ax * x + B * x) + C;
+    uint32_t bits = __float_as_uint(v + RND_MAGIC) & wrap_mask<TIn>();
+    asm("" : "+v"(bits));  // keep LLVM from folding this back into a cvt
+    return __uint_as_float(bits) - 0x1p23f;
+}
+
 // agree_subpixel (agree.hpp:95-191). MAXN >= n bounds the per-lane register arrays
-// (static indices only; t >= n iterations are skipped by wave-uniform branches). The
-// quadratic interpolation is float in both precisions (agree.cuh:221-236).
-template <typename TIn, typename TPrec, int MAXN, bool EXACT>
+// (static indices only). Slots t < LO (the smallest n routed to this bucket) are always
+// live; slots LO <= t < MAXN beyond n are padded with exact no-ops: A = B = C = 0 gives
+// an interpolated 0 (sum unchanged), D0 = 0 and x1 = 0 leave both fma chains unchanged
+// (neither accumulator is ever -0). The quadratic is float in both precisions.
+//
+// The x loop is software-pipelined: one pass over t finishes step k (x1 = IV - m1 and the
+// in-order cov / var fma chains) and interpolates step k+1 into the same IV registers, so
+// every chain op has independent interpolation work beside it and the register footprint
+// is that of one step. nsteps is the host's count of x = -1, -1+step, ... <= 1, accumulated
+// in float exactly as the reference's loop (engine.cpp subpixel_steps).
+template <typename TIn, typename TPrec, int MAXN, int LO>
 __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
     const int col = blockIdx.x * 256 + threadIdx.x;
     const int row = blockIdx.y;
     if (col >= a.cols) return;
     const size_t o = (size_t)row * a.cols + col;
-    const int n = EXACT ? MAXN : a.n;
+    const int n = LO == MAXN ? MAXN : a.n;
     const size_t pp = a.plane_pitch;
     const int d = a.raw[(size_t)row * a.raw_pitch + col];
     const TPrec minvar = (TPrec)a.minvar;
@@ -949,59 +984,43 @@ __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
             const StackReader<TIn> rd0(a.stack0, a.stack_bytes), rd1(a.stack1, a.stack_bytes);
             const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
             // left: mean, centred samples and variance are the same for every x
+            // padded slots re-read plane 0 (in bounds) and are zeroed; int -> float via
+            // small_int_to_float (two full-rate ops instead of a quarter-rate v_cvt_f32_*)
             TPrec D0[MAXN];
             float A[MAXN], B[MAXN], C[MAXN];
             uint32_t s = 0;
 #pragma unroll
-            for (int t = 0; t < MAXN; ++t)
-                if (t < n) {
-                    const uint32_t po = rowoff + (uint32_t)(t * pp);
-                    const uint32_t l = rd0((uint32_t)col, po);
-                    D0[t] = (TPrec)l;
-                    s += l;
-                    const int y0 = (int)rd1((uint32_t)(col1 - 1), po);
-                    const int y1 = (int)rd1((uint32_t)col1, po);
-                    const int y2 = (int)rd1((uint32_t)(col1 + 1), po);
-                    // 0.5f * ( y0 - 2.0f * y1 + y2) ; 0.5f * (-y0 + y2) ; y1
-                    A[t] = 0.5f * (((float)y0 - 2.0f * (float)y1) + (float)y2);
-                    B[t] = 0.5f * (float)(-y0 + y2);
-                    C[t] = (float)y1;
-                }
+            for (int t = 0; t < MAXN; ++t) {
+                const bool live = t < LO || t < n;
+                const uint32_t po = rowoff + (live ? (uint32_t)(t * pp) : 0u);
+                const uint32_t l = rd0((uint32_t)col, po);
+                const int y0 = (int)rd1((uint32_t)(col1 - 1), po);
+                const int y1 = (int)rd1((uint32_t)col1, po);
+                const int y2 = (int)rd1((uint32_t)(col1 + 1), po);
+                // 0.5f * ( y0 - 2.0f * y1 + y2) ; 0.5f * (-y0 + y2) ; y1 -- exact on integers
+                // of this size, so formed in int and converted once
+                A[t] = live ? 0.5f * small_int_to_float(y0 - 2 * y1 + y2) : 0.f;
+                B[t] = live ? 0.5f * small_int_to_float(y2 - y0) : 0.f;
+                C[t] = live ? small_int_to_float(y1) : 0.f;
+                D0[t] = live ? (TPrec)small_int_to_float((int)l) : (TPrec)0;
+                s += live ? l : 0u;
+            }
             const TPrec m0 = div_p((TPrec)s, (TPrec)n);
             TPrec v0 = 0;
 #pragma unroll
-            for (int t = 0; t < MAXN; ++t)
-                if (t < n) {
-                    D0[t] = D0[t] - m0;
-                    v0 = fma_p(D0[t], D0[t], v0);
-                }
+            for (int t = 0; t < MAXN; ++t) {
+                const bool live = t < LO || t < n;
+                D0[t] = live ? D0[t] - m0 : (TPrec)0;
+                v0 = fma_p(D0[t], D0[t], v0);
+            }
             const bool v0_low = a.has_minvar && v0 < minvar;
 
             float best_x = 0.f;
             TPrec best = -1;
             const float step = a.step;
-            for (float x = -1.f; x <= 1.f; x += step) {
-                float IV[MAXN];
-                uint32_t si = 0;
-#pragma unroll
-                for (int t = 0; t < MAXN; ++t)
-                    if (t < n) {
-                        const float ax = A[t] * x;
-                        const float v = (ax * x + B[t] * x) + C[t];
-                        // (TIn)roundevenf(v): the narrowing wraps through int32
-                        const uint32_t iv = (uint32_t)(TIn)(int)__builtin_rintf(v);
-                        IV[t] = (float)iv;
-                        si += iv;
-                    }
-                const TPrec m1 = div_p((TPrec)si, (TPrec)n);
-                TPrec cov = 0, v1 = 0;
-#pragma unroll
-                for (int t = 0; t < MAXN; ++t)
-                    if (t < n) {
-                        const TPrec x1 = (TPrec)IV[t] - m1;
-                        cov = fma_p(D0[t], x1, cov);
-                        v1 = fma_p(x1, x1, v1);
-                    }
+            float x = -1.f;
+            // cov / var of step x, then the reference's argmax (first maximum wins)
+            auto finish = [&](TPrec cov, TPrec v1) {
                 TPrec nxc;
                 if (v0_low || (a.has_minvar && v1 < minvar))
                     nxc = -1;
@@ -1010,6 +1029,69 @@ __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
                 if (best < nxc) {
                     best_x = x;
                     best = nxc;
+                }
+            };
+            float IV[MAXN];
+            float sf[4] = {0.f, 0.f, 0.f, 0.f};  // exact in any order: integers < 2^24
+            if constexpr (MAXN <= 40) {
+                // Software-pipelined: one pass over t finishes step k (x1 = IV - m1 and the
+                // in-order fma chains) and interpolates step k+1 into the same registers.
+#pragma unroll
+                for (int t = 0; t < MAXN; ++t) {
+                    IV[t] = interp_wrapped<TIn>(A[t], B[t], C[t], x);
+                    sf[t & 3] += IV[t];
+                }
+                for (int k = 0; k < a.nsteps; ++k) {
+                    const TPrec m1 = div_p((TPrec)((sf[0] + sf[1]) + (sf[2] + sf[3])), (TPrec)n);
+                    const float xn = x + step;
+                    TPrec cov = 0, v1 = 0;
+                    // two copies of the body: a wave-uniform test inside the unrolled t loop
+                    // becomes one scalar branch per slot and breaks the schedule (measured 3x)
+                    if (k + 1 < a.nsteps) {
+#pragma unroll
+                        for (int t = 0; t < MAXN; ++t) {
+                            TPrec x1 = (TPrec)IV[t] - m1;
+                            if (t >= LO) x1 = t < n ? x1 : (TPrec)0;
+                            cov = fma_p(D0[t], x1, cov);
+                            v1 = fma_p(x1, x1, v1);
+                            IV[t] = interp_wrapped<TIn>(A[t], B[t], C[t], xn);
+                        }
+                        sf[0] = sf[1] = sf[2] = sf[3] = 0.f;
+#pragma unroll
+                        for (int t = 0; t < MAXN; ++t) sf[t & 3] += IV[t];
+                    } else {
+#pragma unroll
+                        for (int t = 0; t < MAXN; ++t) {
+                            TPrec x1 = (TPrec)IV[t] - m1;
+                            if (t >= LO) x1 = t < n ? x1 : (TPrec)0;
+                            cov = fma_p(D0[t], x1, cov);
+                            v1 = fma_p(x1, x1, v1);
+                        }
+                    }
+                    finish(cov, v1);
+                    x = xn;
+                }
+            } else {
+                // One wave/SIMD: the arrays already overflow into AGPRs, so keep IV dead
+                // across the loop's back edge (interpolate at the top of each step).
+                for (int k = 0; k < a.nsteps; ++k) {
+                    sf[0] = sf[1] = sf[2] = sf[3] = 0.f;
+#pragma unroll
+                    for (int t = 0; t < MAXN; ++t) {
+                        IV[t] = interp_wrapped<TIn>(A[t], B[t], C[t], x);
+                        sf[t & 3] += IV[t];
+                    }
+                    const TPrec m1 = div_p((TPrec)((sf[0] + sf[1]) + (sf[2] + sf[3])), (TPrec)n);
+                    TPrec cov = 0, v1 = 0;
+#pragma unroll
+                    for (int t = 0; t < MAXN; ++t) {
+                        TPrec x1 = (TPrec)IV[t] - m1;
+                        if (t >= LO) x1 = t < n ? x1 : (TPrec)0;
+                        cov = fma_p(D0[t], x1, cov);
+                        v1 = fma_p(x1, x1, v1);
+                    }
+                    finish(cov, v1);
+                    x += step;
                 }
             }
             corr = best;
@@ -1037,14 +1119,14 @@ hipError_t launch_transform_w(const TransformArgs& a, int mode, hipStream_t st) 
     if (mode == 0) {
         // descriptor width bounds n: 32 bits -> n <= 9, 64 -> 17, 128 -> 33, 256 -> 65
         const int n = a.n;
-        if (WORDS == 1) return launch_tl<TIn, WORDS, 9>(a, grid, st);
-        if (WORDS == 2) return n <= 12 ? launch_tl<TIn, WORDS, 12>(a, grid, st)
-                                       : launch_tl<TIn, WORDS, 17>(a, grid, st);
-        if (WORDS == 4) return n <= 24 ? launch_tl<TIn, WORDS, 24>(a, grid, st)
-                                       : launch_tl<TIn, WORDS, 33>(a, grid, st);
-        if (n <= 40) return launch_tl<TIn, WORDS, 40>(a, grid, st);
-        if (n <= 48) return launch_tl<TIn, WORDS, 48>(a, grid, st);
-        return launch_tl<TIn, WORDS, 65>(a, grid, st);
+        if constexpr (WORDS == 1) return launch_tl<TIn, WORDS, 9>(a, grid, st);
+        else if constexpr (WORDS == 2) return n <= 12 ? launch_tl<TIn, WORDS, 12>(a, grid, st)
+                                                      : launch_tl<TIn, WORDS, 17>(a, grid, st);
+        else if constexpr (WORDS == 4) return n <= 24 ? launch_tl<TIn, WORDS, 24>(a, grid, st)
+                                                      : launch_tl<TIn, WORDS, 33>(a, grid, st);
+        else if (n <= 40) return launch_tl<TIn, WORDS, 40>(a, grid, st);
+        else if (n <= 48) return launch_tl<TIn, WORDS, 48>(a, grid, st);
+        else return launch_tl<TIn, WORDS, 65>(a, grid, st);
     }
     hipLaunchKernelGGL((transform_kernel<TIn, WORDS, 1>), grid, dim3(256), 0, st, a);
     return hipGetLastError();
@@ -1117,27 +1199,28 @@ hipError_t launch_search_w(const SearchArgs& a, bool nodupes, const SearchGeomet
     return nodupes ? launch_search_n<WORDS, true>(a, g, st) : launch_search_n<WORDS, false>(a, g, st);
 }
 
-template <typename TIn, typename TPrec, int MAXN>
+template <typename TIn, typename TPrec, int MAXN, int LO>
 hipError_t launch_subpixel_m(const AgreeArgs& a, hipStream_t st) {
     dim3 grid((a.cols + 255) / 256, a.rows);
     if (a.n == MAXN)
-        hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN, true>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN, MAXN>), grid, dim3(256), 0, st, a);
     else
-        hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN, false>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN, LO>), grid, dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
 template <typename TIn, typename TPrec>
 hipError_t launch_subpixel_t(const AgreeArgs& a, hipStream_t st) {
     const int n = a.n;
-    if (n <= 8) return launch_subpixel_m<TIn, TPrec, 8>(a, st);
-    if (n <= 16) return launch_subpixel_m<TIn, TPrec, 16>(a, st);
-    if (n <= 24) return launch_subpixel_m<TIn, TPrec, 24>(a, st);
-    if (n <= 33) return launch_subpixel_m<TIn, TPrec, 33>(a, st);
-    if (n <= 40) return launch_subpixel_m<TIn, TPrec, 40>(a, st);
-    if (n <= 48) return launch_subpixel_m<TIn, TPrec, 48>(a, st);
-    if (n <= 56) return launch_subpixel_m<TIn, TPrec, 56>(a, st);
-    if (n <= 65) return launch_subpixel_m<TIn, TPrec, 65>(a, st);
+    if (a.nsteps < 1) return hipErrorInvalidValue;
+    if (n <= 8) return launch_subpixel_m<TIn, TPrec, 8, 2>(a, st);
+    if (n <= 16) return launch_subpixel_m<TIn, TPrec, 16, 9>(a, st);
+    if (n <= 24) return launch_subpixel_m<TIn, TPrec, 24, 17>(a, st);
+    if (n <= 33) return launch_subpixel_m<TIn, TPrec, 33, 25>(a, st);
+    if (n <= 40) return launch_subpixel_m<TIn, TPrec, 40, 34>(a, st);
+    if (n <= 48) return launch_subpixel_m<TIn, TPrec, 48, 41>(a, st);
+    if (n <= 56) return launch_subpixel_m<TIn, TPrec, 56, 49>(a, st);
+    if (n <= 65) return launch_subpixel_m<TIn, TPrec, 65, 57>(a, st);
     return hipErrorInvalidValue;
 }
 

@@ -61,6 +61,7 @@ struct AgreeArgs {
     size_t row_pitch, plane_pitch;
     float threshold;
     float step;             // subpixel only
+    int nsteps;             // subpixel only: x = -1, -1+step, ... <= 1 (subpixel_steps)
     int has_minvar;
     float minvar;           // already scaled by n (reference cpu.cpp:127)
     void* out;              // dense [rows][cols]

@@ -134,9 +134,14 @@ def test_agree_bit_exact(gpu, oracle, n, dt, minvar):
     same(host(corr), rc)
 
 
-@pytest.mark.parametrize("n,dt", [(2, np.uint8), (8, np.uint8), (12, np.uint16), (33, np.uint8),
-                                  (33, np.uint16), (40, np.uint8), (65, np.uint8)])
-@pytest.mark.parametrize("step,minvar", [(0.1, None), (0.25, 1.0), (0.05, None)])
+# n covers exact buckets and padded ones (2, 12, 25, 45, 60: slots n..MAXN-1 are exact
+# no-ops) in both loop structures (pipelined MAXN <= 40, top-of-step above); steps cover
+# 41/20/8 x values, 3 and a single x (step > 2)
+@pytest.mark.parametrize("n,dt", [(2, np.uint8), (8, np.uint8), (12, np.uint16), (25, np.uint8),
+                                  (33, np.uint8), (33, np.uint16), (40, np.uint8),
+                                  (45, np.uint16), (60, np.uint8), (65, np.uint8)])
+@pytest.mark.parametrize("step,minvar", [(0.1, None), (0.25, 1.0), (0.05, None), (0.7, None),
+                                         (2.5, 1.0)])
 def test_subpixel_bit_exact(gpu, oracle, n, dt, step, minvar):
     H, W = 7, 160
     L = random_stack(n, H, W, dt, seed=n + 1)
@@ -292,6 +297,12 @@ def test_errors(gpu):
     s = torch.zeros((8, 4, 4), dtype=torch.uint8, device="cuda")
     with pytest.raises(BicosError, match="subpixel_step"):
         gpu.match(s, s, MatchConfig(subpixel_step=0.0))
+    # x + step == x somewhere in [-1, 1]: the reference loops forever; rejected here
+    with pytest.raises(BicosError, match="too small"):
+        gpu.match(s, s, MatchConfig(nxcorr_threshold=0.5, subpixel_step=1e-9))
+    raw = torch.zeros((4, 4), dtype=torch.int16, device="cuda")
+    with pytest.raises(BicosError, match="too small"):
+        gpu.agree(raw, s, s, 0.5, step=1e-5)
 
 
 def test_pybicos_errors(gpu):

@@ -16,11 +16,25 @@ run() {  # name timeout cmd...
 for step in "$@"; do
     case $step in
         valu) run valu 120 ./build/valu_peak ;;
+        dep) run dep 200 ./build/dep_bench ;;
         smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
         pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
         pytestk) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
         bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
         bench3) run bench3 600 python bench.py --config cfg3 --steps 10 --warmup 2 --no-cpu-baseline ;;
+        ab3|ab2|ab4)  # A/B on one box: current lib vs build/alt.so (same bench, interleaved twice)
+            c=cfg${step#ab}
+            cp libbicos_amd/libbicos_amd.so build/cur.so
+            for k in 1 2; do
+                cp build/cur.so libbicos_amd/libbicos_amd.so
+                run ${step}_cur$k 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline
+                cp build/alt.so libbicos_amd/libbicos_amd.so
+                run ${step}_alt$k 300 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline
+            done
+            cp build/cur.so libbicos_amd/libbicos_amd.so ;;
+        subpix) run subpix 300 python tools/subpix_bench.py ;;
+        subpixs) run subpixs 300 python tools/subpix_bench.py --ns 16,33 --steps 0.5,0.2,0.1,0.05 ;;
+        subpix16) run subpix16 300 python tools/subpix_bench.py --depth 2 --ns 8,16,24,33 ;;
         bench4) run bench4 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline ;;
         bench5) run bench5 600 python bench.py --config cfg5 --steps 10 --warmup 2 --no-cpu-baseline ;;
         sweep) run sweep 600 python tools/search_sweep.py --variants 16:2:8:2,18:2:8:2,16:2:8:1,18:2:8:1,18:4:8:2,17:2:8:2 ;;
@@ -30,6 +44,7 @@ for step in "$@"; do
         sweep48) run sweep48 600 python tools/search_sweep.py --rows 384 --variants 0:0:0:0,16:2:8:2,16:2:8:4,16:2:8:8 && python tools/search_sweep.py --rows 768 --variants 0:0:0:0,16:2:8:1,16:2:8:2,16:2:8:4 && python tools/search_sweep.py --config cfg5 --rows 270 --variants 0:0:0:0,16:2:8:4,16:2:8:8 ;;
         sweep5) run sweep5 600 python tools/search_sweep.py --config cfg5 --rows 270 --variants 0:0:0:0,16:2:8:1,16:2:8:2,16:2:8:4 ;;
         rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --steps 5 --warmup 1 --no-cpu-baseline ;;
+        pmcsub) run pmcsub 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmcsub -o run --output-format csv -- python bench.py --config cfg3 --steps 2 --warmup 1 --no-cpu-baseline --kernel-reps 1 ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
         pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 2 ;;
         pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 2 ;;

@@ -38,6 +38,19 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
             if (OP == 13) asm volatile("v_bcnt_u32_b32 %0, %1, %0" : "+v"(v[c]) : "s"(seed));
             if (OP == 14) asm volatile("v_mov_b32 %0, %1" : "=v"(v[c]) : "v"(w[c]));
             if (OP == 15) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
+            if (OP == 17) asm volatile("v_add_f32 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 18) asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 19) asm volatile("v_cvt_f32_ubyte0 %0, %1" : "=v"(v[c]) : "v"(w[c] ^ v[c]));
+            if (OP == 20) asm volatile("v_pk_fma_f32 %0, %1, %1, %0" : "+v"(*(uint64_t*)&v[c & ~1]) : "v"(*(uint64_t*)&w[c & ~1]));
+            if (OP == 21) asm volatile("v_rndne_f32 %0, %0" : "+v"(v[c]));
+            if (OP == 22) asm volatile("v_cvt_i32_f32 %0, %0" : "+v"(v[c]));
+            if (OP == 23) asm volatile("v_sub_f32 %0, %1, %0" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 24) asm volatile("v_fma_mix_f32 %0, %1, %0, %0 op_sel_hi:[1,0,0]" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 25) asm volatile("v_pk_add_f16 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 26) asm volatile("v_cvt_f32_f16 %0, %1" : "=v"(v[c]) : "v"(w[c] ^ v[c]));
+            if (OP == 27) asm volatile("v_or_b32_sdwa %0, %1, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 28) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 29) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(*(uint64_t*)&v[c & ~1]) : "v"(*(uint64_t*)&w[c & ~1]));
             if (OP == 16) {  // the search loop's 128-bit mix per pair: 4 xor, 4 bcnt, lshl_or, med3, min
                 uint32_t t0, t1, t2, t3, cst, key;
                 asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t0) : "v"(v[c]), "v"(w[c]));
@@ -112,6 +125,19 @@ int main() {
     run<14>("v_mov_b32", out, grid);
     run<15>("v_xad_u32", out, grid);
     run<16>("search_mix_128(11 ops/pair)", out, grid);
+    run<17>("v_add_f32", out, grid);
+    run<18>("v_fmac_f32", out, grid);
+    run<19>("v_xor+v_cvt_f32_ubyte0 (2 ops)", out, grid);
+    run<20>("v_pk_fma_f32 (per instr)", out, grid);
+    run<21>("v_rndne_f32", out, grid);
+    run<22>("v_cvt_i32_f32", out, grid);
+    run<23>("v_sub_f32", out, grid);
+    run<24>("v_fma_mix_f32 (f16 lo operand)", out, grid);
+    run<25>("v_pk_add_f16", out, grid);
+    run<26>("v_xor+v_cvt_f32_f16 (2 ops)", out, grid);
+    run<27>("v_or_b32_sdwa byte0", out, grid);
+    run<28>("v_mul_f32", out, grid);
+    run<29>("v_pk_mul_f32 (per instr)", out, grid);
     hipFree(out);
     return 0;
 }
