@@ -113,6 +113,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target wall time of the CPU baseline sample")
     ap.add_argument("--kernel-reps", type=int, default=10)
+    ap.add_argument("--no-host-path", action="store_true",
+                    help="skip the end-to-end host-buffer measurement (rank 0, N=1)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo = rehearsal of the N>1 "
                          "path with several ranks sharing one GPU (not a measurement)")
@@ -304,6 +306,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(C, args.cpu_seconds)
+    hp = None
+    if rank == 0 and world == 1 and not args.no_host_path:
+        hp = host_path(C, mcfg, reps=5)
 
     if rank == 0:
         line = {
@@ -328,10 +333,52 @@ def main():
             },
             "roofline": roof,
             "cpu_baseline": cpu,
+            "host_path": hp,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def host_path(C, mcfg, reps):
+    """The same match from host numpy stacks to host maps (bicos_match_host: what
+    BICOS_Match / pybicos.match run), PCIe transfers included. Reported beside the metric,
+    never as `value` (SURVEY.md s8 d: end-to-end incl. H2D/D2H separately)."""
+    import ctypes
+    import numpy as np
+    from libbicos_amd import _lib
+    from libbicos_amd.synthetic import stereo_stack
+
+    n, H, W = C["n"], C["H"], C["W"]
+    L, R = stereo_stack(n, H, W, np.uint8)
+    left = [L[t].copy() for t in range(n)]  # separately allocated images, like cv2 reads
+    right = [R[t].copy() for t in range(n)]
+    p0 = (ctypes.c_void_p * n)(*[a.ctypes.data for a in left])
+    p1 = (ctypes.c_void_p * n)(*[a.ctypes.data for a in right])
+    cfgc, has = mcfg.to_c()
+    disp = np.empty((H, W), np.float32 if has else np.int16)
+    corr = np.empty((H, W), np.float64 if mcfg.precision else np.float32)
+    lib = _lib.lib()
+
+    def once():
+        t0 = time.perf_counter()
+        _lib.check(lib.bicos_match_host(None, p0, p1, n, H, W, 0, 1, ctypes.byref(cfgc), has,
+                                        disp.ctypes.data, corr.ctypes.data if has else None),
+                   "bicos_match_host")
+        return time.perf_counter() - t0
+
+    once()
+    ts = [once() for _ in range(reps)]
+    t = float(sorted(ts)[len(ts) // 2])
+    return {
+        "ms_per_match": round(t * 1e3, 3),
+        "value": round(H * W / t / 1e6, 1),
+        "unit": "Mpix/s",
+        "h2d_bytes": int(L.nbytes + R.nbytes),
+        "d2h_bytes": int(disp.nbytes + (corr.nbytes if has else 0)),
+        "what": "host numpy stacks (separate images) -> host maps via bicos_match_host "
+                "(banded pinned upload overlapped with the match), median of %d" % reps,
+    }
 
 
 def cpu_baseline(C, seconds):

@@ -97,6 +97,9 @@ const char* bicos_last_error(void);
 typedef struct bicos_engine bicos_engine;
 
 int bicos_engine_create(int device, bicos_engine** out);
+/* The process-wide engine of `device` that BICOS_Match, bicos_match_host(NULL, ...) and
+ * BICOS::match use (created on first use; bicos_engine_destroy ignores it). NULL on error. */
+bicos_engine* bicos_engine_default(int device);
 void bicos_engine_destroy(bicos_engine* e);
 
 /* Search-kernel tuning for this engine (0 = automatic for each argument):
@@ -131,6 +134,21 @@ int bicos_match_device(bicos_engine* e, const void* stack0, const void* stack1, 
                        int cols, size_t row_pitch, size_t plane_pitch, int depth,
                        const BicosConfig* cfg, int has_nxcorr, void* disparity, void* corrmap,
                        void* stream);
+
+/*
+ * Full match on host buffers (the reference's cv::Mat path; what BICOS_Match and
+ * pybicos.match run). Synchronous.
+ *   e             : engine, or NULL for the current device's default engine
+ *   stack0/stack1 : n host image pointers each (any addresses), rows x cols, `step` bytes
+ *                   per row (0 = dense), u8 (depth 1) or u16 (depth 2)
+ *   disparity     : host, rows*cols dense, int16 or float32 per bicos_output_type
+ *   corrmap       : host, rows*cols dense float32 (float64 for DOUBLE), or NULL
+ * The stacks are uploaded in row bands through pinned staging on a copy stream while the
+ * bands already uploaded are matched; the maps are written straight into the buffers.
+ */
+int bicos_match_host(bicos_engine* e, const void* const* stack0, const void* const* stack1, int n,
+                     int rows, int cols, size_t step, int depth, const BicosConfig* cfg,
+                     int has_nxcorr, void* disparity, void* corrmap);
 
 /* Stage entry points (tests, benchmarks, custom pipelines). Same conventions.
  * desc buffers: rows x desc_pitch uint32 with desc_pitch = bicos_desc_pitch(cols, words). */

@@ -55,8 +55,8 @@ class BicosResult(ctypes.Structure):
 EXPORTS = (
     "BICOS_CreateDefaultConfig", "BICOS_FreeConfig", "BICOS_FreeResult", "BICOS_Match",
     "BICOS_InvalidDisparityFloat", "BICOS_InvalidDisparityInt16", "bicos_last_error",
-    "bicos_engine_create", "bicos_engine_destroy", "bicos_engine_tune", "bicos_descriptor_words", "bicos_output_type",
-    "bicos_match_device", "bicos_desc_pitch", "bicos_transform_device", "bicos_search_device",
+    "bicos_engine_create", "bicos_engine_default", "bicos_engine_destroy", "bicos_engine_tune", "bicos_descriptor_words", "bicos_output_type",
+    "bicos_match_device", "bicos_match_host", "bicos_desc_pitch", "bicos_transform_device", "bicos_search_device",
     "bicos_agree_device", "bicos_subpixel_device", "bicos_build_info",
 )
 
@@ -106,6 +106,8 @@ def lib() -> ctypes.CDLL:
     L.bicos_last_error.argtypes = []
     L.bicos_engine_create.argtypes = [I, ctypes.POINTER(P)]
     L.bicos_engine_create.restype = I
+    L.bicos_engine_default.argtypes = [I]
+    L.bicos_engine_default.restype = P
     L.bicos_engine_destroy.argtypes = [P]
     L.bicos_engine_destroy.restype = None
     L.bicos_engine_tune.argtypes = [P, I, I, I, I]
@@ -117,6 +119,8 @@ def lib() -> ctypes.CDLL:
     L.bicos_match_device.argtypes = [P, P, P, I, I, I, Z, Z, I, ctypes.POINTER(BicosConfig), I,
                                      P, P, P]
     L.bicos_match_device.restype = I
+    L.bicos_match_host.argtypes = [P, PP, PP, I, I, I, Z, I, ctypes.POINTER(BicosConfig), I, P, P]
+    L.bicos_match_host.restype = I
     L.bicos_desc_pitch.argtypes = [I, I]
     L.bicos_desc_pitch.restype = Z
     L.bicos_transform_device.argtypes = [P, I, I, I, Z, Z, I, I, I, P, P]

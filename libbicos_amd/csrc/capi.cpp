@@ -82,19 +82,44 @@ BicosResult* BICOS_Match(void** stack0_data, int* stack0_rows, int* stack0_cols,
         for (int i = 0; i < stack1_size; ++i)
             s1.emplace_back(stack1_rows[i], stack1_cols[i], stack1_types[i], stack1_data[i]);
 
-        BICOS::Image disparity, corrmap;
-        BICOS::match(s0, s1, disparity, convert_config(config), &corrmap);
-
+        const BICOS::Config cc = convert_config(config);
         result = (BicosResult*)std::calloc(1, sizeof(BicosResult));
         if (!result) throw BICOS::Exception("out of host memory");
+        // The result buffers are malloc'd as in the reference (pybicos_c.cpp:176,192) and
+        // handed to BICOS::match as views, which it fills in place (Image::create keeps a
+        // buffer of the right size and type), so nothing is copied after the download.
+        BICOS::Image disparity, corrmap;
+        if (stack0_size > 0 && stack0_rows[0] > 0 && stack0_cols[0] > 0) {
+            const int rows = stack0_rows[0], cols = stack0_cols[0];
+            const int dtype = cc.nxcorr_threshold ? BICOS::F32 : BICOS::S16;
+            const int ctype = cc.precision == BICOS::Precision::DOUBLE ? BICOS::F64 : BICOS::F32;
+            const size_t px = (size_t)rows * cols;
+            result->disparity_data = std::malloc(px * BICOS::Image::elem_size(dtype));
+            result->corrmap_data = std::malloc(px * BICOS::Image::elem_size(ctype));
+            if (!result->disparity_data || !result->corrmap_data)
+                throw BICOS::Exception("out of host memory");
+            disparity = BICOS::Image(rows, cols, dtype, result->disparity_data);
+            corrmap = BICOS::Image(rows, cols, ctype, result->corrmap_data);
+        }
+        BICOS::match(s0, s1, disparity, cc, &corrmap);
+
+        // (only if match chose different buffers, e.g. empty images)
+        if (disparity.data() != result->disparity_data) {
+            std::free(result->disparity_data);
+            result->disparity_data = nullptr;
+            result->disparity_data = copy_out(disparity);
+        }
+        if (corrmap.data() != result->corrmap_data) {
+            std::free(result->corrmap_data);
+            result->corrmap_data = nullptr;
+            result->corrmap_data = copy_out(corrmap);
+        }
         result->disparity_rows = disparity.rows();
         result->disparity_cols = disparity.cols();
         result->disparity_type = disparity.type();
-        result->disparity_data = copy_out(disparity);
         result->corrmap_rows = corrmap.rows();
         result->corrmap_cols = corrmap.cols();
         result->corrmap_type = corrmap.type();
-        result->corrmap_data = copy_out(corrmap);
         return result;
     } catch (const std::exception& e) {
         bicos_impl::set_error(BICOS_E_ARG, e.what());

@@ -5,6 +5,9 @@
 //                                 backend entry impl::cpu::match (src/impl/cpu.cpp:100-159)
 #include "engine.hpp"
 
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -152,6 +155,14 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) + (consistency ? 2 * map16 : 0);
     int rc = reserve(e->ws, e->ws_bytes, need, e->device);
     if (rc) return rc;
+    // order against earlier users of ws / stage on other streams; mark our use on exit
+    rc = check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent");
+    if (rc) return rc;
+    struct MarkUse {
+        hipEvent_t ev;
+        hipStream_t st;
+        ~MarkUse() { (void)hipEventRecord(ev, st); }
+    } mark{e->ws_ready, st};
     char* p = (char*)e->ws;
     uint32_t* d0 = (uint32_t*)p;
     p += desc_bytes;
@@ -213,16 +224,236 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     return rc;
 }
 
+// ------------------------------------------------------- host-buffer pipeline
+
+HostPool::HostPool(int threads) {
+    for (int i = 1; i < threads; ++i) workers_.emplace_back([this] { loop(); });
+}
+
+HostPool::~HostPool() {
+    {
+        std::lock_guard<std::mutex> g(m_);
+        stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+}
+
+void HostPool::loop() {
+    unsigned seen = 0;
+    std::unique_lock<std::mutex> lk(m_);
+    for (;;) {
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+        ++active_;
+        while (next_ < tasks_) {
+            const int i = next_++;
+            const std::function<void(int)>* f = job_;
+            lk.unlock();
+            (*f)(i);
+            lk.lock();
+        }
+        if (--active_ == 0) done_.notify_all();
+    }
+}
+
+void HostPool::run(int tasks, const std::function<void(int)>& f) {
+    std::unique_lock<std::mutex> lk(m_);
+    job_ = &f;
+    tasks_ = tasks;
+    next_ = 0;
+    ++gen_;
+    cv_.notify_all();
+    ++active_;
+    while (next_ < tasks_) {
+        const int i = next_++;
+        lk.unlock();
+        f(i);
+        lk.lock();
+    }
+    --active_;
+    done_.wait(lk, [&] { return active_ == 0; });
+    job_ = nullptr;
+    tasks_ = 0;
+}
+
+int match_host(bicos_engine* e, const void* const* p0, const size_t* steps0,
+               const void* const* p1, const size_t* steps1, int n, int rows, int cols,
+               int depth, const BicosConfig& cfg, bool has_nxcorr, float threshold, void* disp,
+               void* corr) {
+    if (!e) return fail(BICOS_E_ARG, "null engine");
+    if (n < 2) return fail(BICOS_E_ARG, "need at least two images");
+    if (depth != 1 && depth != 2)
+        return fail(BICOS_E_ARG, "bad input depths, only CV_8UC1 and CV_16UC1 are supported");
+    if (rows < 0 || cols < 0) return fail(BICOS_E_ARG, "negative image size");
+    hipStream_t cs = e->own_stream, ks = e->copy_stream;
+    if (rows == 0 || cols == 0)  // validates the configuration, no work
+        return match_device(e, nullptr, nullptr, n, rows, cols, (size_t)cols,
+                            (size_t)rows * cols, depth, cfg, has_nxcorr, threshold, disp, corr,
+                            cs);
+    if (!p0 || !p1 || !disp) return fail(BICOS_E_ARG, "null buffer");
+    const size_t row_bytes = (size_t)cols * depth;
+    for (int t = 0; t < n; ++t) {
+        if (!p0[t] || !p1[t]) return fail(BICOS_E_ARG, "null image");
+        if ((steps0 && steps0[t] < row_bytes) || (steps1 && steps1[t] < row_bytes))
+            return fail(BICOS_E_ARG, "image step smaller than a row");
+    }
+
+    // Transfers (measured, tools/host_bench.py): a thread pool gathers each band of the
+    // caller's images into a pinned slot and one DMA per band uploads it (5-7 ms per cfg2
+    // match, PCIe-bound: 207 MB at 35-42 GB/s while the gathers run; pageable
+    // hipMemcpy2DAsync per band and plane: ~11 ms). The maps come down in one copy at the
+    // end (band-wise pinned downloads measured no faster).
+    // Row bands (every stage is row-local): upload of band b+1 overlaps the
+    // match of band b; ~8 bands keep the pipeline tail short without starving the search.
+    const int want = rows >= 1024 ? 8 : rows >= 256 ? 4 : rows >= 64 ? 2 : 1;
+    const int band_rows = (rows + want - 1) / want;
+    const int B = (rows + band_rows - 1) / band_rows;
+    const int K = B > 1 ? 3 : 1;  // pinned slots in flight
+    const size_t band_bytes = 2 * (size_t)n * band_rows * row_bytes;
+    const size_t dsz = has_nxcorr ? 4 : 2, csz = cfg.precision ? 8 : 4;
+    const size_t out_off = align_up((size_t)B * band_bytes);
+    const size_t corr_off = out_off + align_up((size_t)rows * cols * dsz);
+    const size_t total = corr_off + (corr ? (size_t)rows * cols * csz : 0);
+    int rc = reserve(e->stage, e->stage_bytes, total, e->device);
+    if (rc) return rc;
+    if (e->pinned_bytes < (size_t)K * band_bytes) {
+        if (e->pinned) (void)hipHostFree(e->pinned);
+        e->pinned = nullptr;
+        e->pinned_bytes = 0;
+        rc = check_hip(hipHostMalloc(&e->pinned, (size_t)K * band_bytes, hipHostMallocDefault),
+                       "hipHostMalloc(staging)");
+        if (rc) return rc;
+        e->pinned_bytes = (size_t)K * band_bytes;
+    }
+    const size_t disp_bytes = (size_t)rows * cols * dsz;
+    while ((int)e->events.size() < B) {
+        hipEvent_t ev;
+        rc = check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+        if (rc) return rc;
+        e->events.push_back(ev);
+    }
+    if (!e->pool) {
+        // gather threads (BICOS_HOST_THREADS, default 8): the gathers compete with the DMA
+        // for host memory bandwidth; 16 threads measured slower than 3-8 (tools/host_bench.py)
+        const unsigned hw = std::thread::hardware_concurrency();
+        const char* th = std::getenv("BICOS_HOST_THREADS");
+        const unsigned cap = th ? (unsigned)std::max(1, std::atoi(th)) : 8u;
+        e->pool.reset(new HostPool((int)std::max(1u, std::min(cap, hw ? hw : 1u))));
+    }
+
+    // BICOS_HOST_TRACE=1: per-phase host timestamps on stderr (tools/host_bench.py)
+    static const bool trace = std::getenv("BICOS_HOST_TRACE") != nullptr;
+    const auto t_start = std::chrono::steady_clock::now();
+    auto stamp = [&](const char* what, int b) {
+        if (!trace) return;
+        const double us = std::chrono::duration<double, std::micro>(
+                              std::chrono::steady_clock::now() - t_start).count();
+        std::fprintf(stderr, "[bicos host] %8.1f us  %s %d\n", us, what, b);
+    };
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> dma_ev;
+    // earlier calls (possibly on other streams) may still read the stage / workspace
+    rc = check_hip(hipStreamWaitEvent(ks, e->ws_ready, 0), "hipStreamWaitEvent");
+    if (rc) return rc;
+    char* dev = (char*)e->stage;
+    char* dev_disp = dev + out_off;
+    char* dev_corr = corr ? dev + corr_off : nullptr;
+    for (int b = 0; b < B && rc == BICOS_OK; ++b) {
+        const int r0 = b * band_rows;
+        const int br = std::min(band_rows, rows - r0);
+        const size_t plane = (size_t)br * row_bytes;
+        char* slot = (char*)e->pinned + (size_t)(b % K) * band_bytes;
+        if (b >= K) {
+            rc = check_hip(hipEventSynchronize(e->events[b - K]), "hipEventSynchronize");
+            if (rc) break;
+        }
+        char* band = dev + (size_t)b * band_bytes;
+        // 2n planes -> slot [2n][br][cols], dense
+        const std::function<void(int)> copy = [&](int i) {
+            const bool right = i >= n;
+            const int t = right ? i - n : i;
+            const size_t step = right ? (steps1 ? steps1[t] : row_bytes)
+                                      : (steps0 ? steps0[t] : row_bytes);
+            const char* src = (const char*)(right ? p1[t] : p0[t]) + (size_t)r0 * step;
+            char* dst = slot + (size_t)i * plane;
+            if (step == row_bytes) {
+                std::memcpy(dst, src, plane);
+            } else {
+                for (int r = 0; r < br; ++r)
+                    std::memcpy(dst + (size_t)r * row_bytes, src + (size_t)r * step, row_bytes);
+            }
+        };
+        stamp("slot free", b);
+        e->pool->run(2 * n, copy);
+        stamp("gathered", b);
+        hipEvent_t t0 = nullptr, t1 = nullptr;
+        if (trace) {
+            (void)hipEventCreate(&t0);
+            (void)hipEventCreate(&t1);
+            (void)hipEventRecord(t0, ks);
+        }
+        rc = check_hip(hipMemcpyAsync(band, slot, 2 * (size_t)n * plane, hipMemcpyHostToDevice, ks),
+                       "stack upload");
+        if (trace) {
+            (void)hipEventRecord(t1, ks);
+            dma_ev.push_back({t0, t1});
+        }
+        if (!rc) rc = check_hip(hipEventRecord(e->events[b], ks), "hipEventRecord");
+        if (!rc) rc = check_hip(hipStreamWaitEvent(cs, e->events[b], 0), "hipStreamWaitEvent");
+        if (!rc)
+            rc = match_device(e, band, band + (size_t)n * plane, n, br, cols, (size_t)cols,
+                              (size_t)br * cols, depth, cfg, has_nxcorr, threshold,
+                              dev_disp + (size_t)r0 * cols * dsz,
+                              dev_corr ? dev_corr + (size_t)r0 * cols * csz : nullptr, cs);
+    }
+    stamp("bands queued", B);
+    if (trace) {
+        (void)hipStreamSynchronize(cs);
+        stamp("bands matched", B);
+    }
+    if (!rc)
+        rc = check_hip(hipMemcpyAsync(disp, dev_disp, disp_bytes, hipMemcpyDeviceToHost, cs),
+                       "download");
+    if (!rc && corr)
+        rc = check_hip(hipMemcpyAsync(corr, dev_corr, (size_t)rows * cols * csz,
+                                      hipMemcpyDeviceToHost, cs),
+                       "download");
+    // drain both streams whatever happened: the slots and the stage are reused next call
+    const int r1 = check_hip(hipStreamSynchronize(ks), "hipStreamSynchronize");
+    const int r2 = check_hip(hipStreamSynchronize(cs), "hipStreamSynchronize");
+    stamp("downloaded", B);
+    for (size_t i = 0; i < dma_ev.size(); ++i) {
+        float ms = 0.f;
+        (void)hipEventElapsedTime(&ms, dma_ev[i].first, dma_ev[i].second);
+        std::fprintf(stderr, "[bicos host] dma %zu: %.3f ms = %.1f GB/s\n", i, ms,
+                     band_bytes / (ms * 1e6));
+        (void)hipEventDestroy(dma_ev[i].first);
+        (void)hipEventDestroy(dma_ev[i].second);
+    }
+    return rc ? rc : (r1 ? r1 : r2);
+}
+
+namespace {
+std::mutex g_engines_lock;
+std::map<int, bicos_engine*> g_engines;
+}  // namespace
+
 bicos_engine* default_engine(int device) {
-    static std::mutex m;
-    static std::map<int, bicos_engine*> engines;
-    std::lock_guard<std::mutex> g(m);
-    auto it = engines.find(device);
-    if (it != engines.end()) return it->second;
+    std::lock_guard<std::mutex> g(g_engines_lock);
+    auto it = g_engines.find(device);
+    if (it != g_engines.end()) return it->second;
     bicos_engine* e = nullptr;
     if (bicos_engine_create(device, &e) != BICOS_OK) return nullptr;
-    engines[device] = e;
+    g_engines[device] = e;
     return e;
+}
+
+bool is_default_engine(const bicos_engine* e) {
+    std::lock_guard<std::mutex> g(g_engines_lock);
+    for (const auto& kv : g_engines)
+        if (kv.second == e) return true;
+    return false;
 }
 
 }  // namespace bicos_impl
@@ -259,8 +490,17 @@ int bicos_engine_create(int device, bicos_engine** out) {
         cus > 0)
         e->cus = cus;
     rc = check_hip(hipStreamCreateWithFlags(&e->own_stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (!rc)
+        rc = check_hip(hipStreamCreateWithFlags(&e->copy_stream, hipStreamNonBlocking),
+                       "hipStreamCreate");
+    if (!rc)
+        rc = check_hip(hipEventCreateWithFlags(&e->ws_ready, hipEventDisableTiming),
+                       "hipEventCreate");
     (void)hipSetDevice(cur);
     if (rc) {
+        if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+        if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
+    if (e->ws_ready) (void)hipEventDestroy(e->ws_ready);
         delete e;
         return rc;
     }
@@ -268,15 +508,22 @@ int bicos_engine_create(int device, bicos_engine** out) {
     return BICOS_OK;
 }
 
+bicos_engine* bicos_engine_default(int device) { return default_engine(device); }
+
 void bicos_engine_destroy(bicos_engine* e) {
     if (!e) return;
+    if (is_default_engine(e)) return;  // the process-wide engines live until exit
     int cur = 0;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(e->device);
     (void)hipDeviceSynchronize();
     if (e->ws) (void)hipFree(e->ws);
     if (e->stage) (void)hipFree(e->stage);
+    if (e->pinned) (void)hipHostFree(e->pinned);
+    for (hipEvent_t ev : e->events) (void)hipEventDestroy(ev);
+    e->pool.reset();
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
+    if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
     (void)hipSetDevice(cur);
     delete e;
 }
@@ -328,6 +575,32 @@ int bicos_match_device(bicos_engine* e, const void* stack0, const void* stack1, 
         const float thr = cfg->nxcorr_threshold >= 0 ? cfg->nxcorr_threshold : 0.5f;
         return match_device(e, stack0, stack1, n, rows, cols, row_pitch, plane_pitch, depth, *cfg,
                             has_nxcorr != 0, thr, disparity, corrmap, (hipStream_t)stream);
+    } catch (const std::exception& ex) {
+        return fail(BICOS_E_INTERNAL, ex.what());
+    } catch (...) {
+        return fail(BICOS_E_INTERNAL, "unknown exception");
+    }
+}
+
+int bicos_match_host(bicos_engine* e, const void* const* stack0, const void* const* stack1, int n,
+                     int rows, int cols, size_t step, int depth, const BicosConfig* cfg,
+                     int has_nxcorr, void* disparity, void* corrmap) {
+    if (!cfg) return fail(BICOS_E_ARG, "null config");
+    if (n < 0) return fail(BICOS_E_ARG, "negative stack size");
+    try {
+        if (!e) {
+            int dev = 0;
+            int rc = check_hip(hipGetDevice(&dev), "hipGetDevice");
+            if (rc) return rc;
+            e = default_engine(dev);
+            if (!e) return BICOS_E_HIP;  // bicos_last_error says why
+        }
+        std::lock_guard<std::mutex> g(e->lock);
+        // reference src/pybicos_c.cpp:59-61: a negative threshold keeps the default 0.5
+        const float thr = cfg->nxcorr_threshold >= 0 ? cfg->nxcorr_threshold : 0.5f;
+        const std::vector<size_t> steps((size_t)n, step ? step : (size_t)(cols > 0 ? cols : 0) * depth);
+        return match_host(e, stack0, steps.data(), stack1, steps.data(), n, rows, cols, depth, *cfg,
+                          has_nxcorr != 0, thr, disparity, corrmap);
     } catch (const std::exception& ex) {
         return fail(BICOS_E_INTERNAL, ex.what());
     } catch (...) {
@@ -463,7 +736,12 @@ Image::Image(int rows, int cols, int type, void* data, size_t step, Memory mem)
 }
 
 void Image::create(int rows, int cols, int type, Memory mem) {
-    if (_owner && _rows == rows && _cols == cols && _type == type && _mem == mem) return;
+    // like cv::Mat::create: a no-op when the header already describes a dense buffer of this
+    // size and type (owned or a view of the caller's memory), so results can be written
+    // straight into caller-provided buffers
+    if (_data && _rows == rows && _cols == cols && _type == type && _mem == mem &&
+        _step == (size_t)cols * elem_size(type))
+        return;
     const size_t step = (size_t)cols * elem_size(type);
     const size_t bytes = step * rows;
     void* p = nullptr;
@@ -537,6 +815,27 @@ void match(const std::vector<Image>& stack0, const std::vector<Image>& stack1, I
     if (!e) throw Exception(bicos_impl::last_error());
     std::lock_guard<std::mutex> g(e->lock);
     hipStream_t st = mem == Memory::Host ? e->own_stream : stream;
+    const int dtype = has_nxcorr ? F32 : S16;
+    const bool dbl = c.precision != 0;
+    const bool want_corr = corrmap && has_nxcorr;
+
+    if (mem == Memory::Host) {
+        // banded, pipelined upload -> match -> download (bicos_impl::match_host)
+        std::vector<const void*> p0(n), p1(n);
+        std::vector<size_t> st0(n), st1(n);
+        for (size_t t = 0; t < n; ++t) {
+            p0[t] = stack0[t].data();
+            p1[t] = stack1[t].data();
+            st0[t] = stack0[t].step();
+            st1[t] = stack1[t].step();
+        }
+        disparity.create(rows, cols, dtype, Memory::Host);
+        if (want_corr) corrmap->create(rows, cols, dbl ? F64 : F32, Memory::Host);
+        throw_rc(bicos_impl::match_host(e, p0.data(), st0.data(), p1.data(), st1.data(), (int)n,
+                                        rows, cols, depth, c, has_nxcorr, c.nxcorr_threshold,
+                                        disparity.data(), want_corr ? corrmap->data() : nullptr));
+        return;
+    }
 
     // the planar device stacks the kernels read
     const size_t elem = (size_t)depth;
@@ -559,17 +858,16 @@ void match(const std::vector<Image>& stack0, const std::vector<Image>& stack1, I
     };
     size_t rp0 = 0, pp0 = 0, rp1 = 0, pp1 = 0;
     const size_t plane_bytes = (size_t)rows * cols * elem;
-    if (mem == Memory::Device && uniform(stack0, rp0, pp0) && uniform(stack1, rp1, pp1) &&
-        rp0 == rp1 && pp0 == pp1) {
+    if (uniform(stack0, rp0, pp0) && uniform(stack1, rp1, pp1) && rp0 == rp1 && pp0 == pp1) {
         s0 = stack0[0].data();
         s1 = stack1[0].data();
         row_pitch = rp0;
         plane_pitch = pp0;
     } else if (rows > 0 && cols > 0) {
         throw_rc(reserve(e->stage, e->stage_bytes, 2 * n * plane_bytes, e->device));
+        throw_rc(check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent"));
         char* dst = (char*)e->stage;
-        const hipMemcpyKind kind =
-            mem == Memory::Host ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+        const hipMemcpyKind kind = hipMemcpyDeviceToDevice;
         for (size_t t = 0; t < n; ++t) {
             throw_rc(check_hip(hipMemcpy2DAsync(dst + t * plane_bytes, cols * elem,
                                                 stack0[t].data(), stack0[t].step(), cols * elem,
@@ -584,39 +882,11 @@ void match(const std::vector<Image>& stack0, const std::vector<Image>& stack1, I
         s1 = dst + n * plane_bytes;
     }
 
-    const int dtype = has_nxcorr ? F32 : S16;
-    const bool dbl = c.precision != 0;
-    Image ddisp, dcorr;
-    const bool want_corr = corrmap && has_nxcorr;
-    if (mem == Memory::Device) {
-        disparity.create(rows, cols, dtype, Memory::Device);
-        if (want_corr) corrmap->create(rows, cols, dbl ? F64 : F32, Memory::Device);
-        ddisp = disparity;
-        if (want_corr) dcorr = *corrmap;
-    } else {
-        ddisp.create(rows, cols, dtype, Memory::Device);
-        if (want_corr) dcorr.create(rows, cols, dbl ? F64 : F32, Memory::Device);
-    }
+    disparity.create(rows, cols, dtype, Memory::Device);
+    if (want_corr) corrmap->create(rows, cols, dbl ? F64 : F32, Memory::Device);
     throw_rc(bicos_impl::match_device(e, s0, s1, (int)n, rows, cols, row_pitch, plane_pitch, depth,
-                                      c, has_nxcorr, c.nxcorr_threshold, ddisp.data(),
-                                      want_corr ? dcorr.data() : nullptr,
-                                      st));
-    if (mem == Memory::Host) {
-        disparity.create(rows, cols, dtype, Memory::Host);
-        if (want_corr) corrmap->create(rows, cols, dbl ? F64 : F32, Memory::Host);
-        if (rows > 0 && cols > 0) {
-            throw_rc(check_hip(hipMemcpyAsync(disparity.data(), ddisp.data(),
-                                              (size_t)rows * cols * Image::elem_size(dtype),
-                                              hipMemcpyDeviceToHost, st),
-                               "download"));
-            if (want_corr)
-                throw_rc(check_hip(hipMemcpyAsync(corrmap->data(), dcorr.data(),
-                                                  (size_t)rows * cols * (dbl ? 8 : 4),
-                                                  hipMemcpyDeviceToHost, st),
-                                   "download"));
-        }
-        throw_rc(check_hip(hipStreamSynchronize(st), "hipStreamSynchronize"));
-    }
+                                      c, has_nxcorr, c.nxcorr_threshold, disparity.data(),
+                                      want_corr ? corrmap->data() : nullptr, st));
 }
 
 }  // namespace BICOS

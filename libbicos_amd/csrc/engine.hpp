@@ -7,11 +7,38 @@
 
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
+#include <functional>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
+#include <vector>
 
 #include "../../include/bicos_c.h"
 #include "kernels.hpp"
+
+namespace bicos_impl {
+// Small persistent pool for the host-side copies of the host-buffer pipeline: run(k, f)
+// calls f(0..k-1), the caller taking part, and returns when all have finished.
+class HostPool {
+  public:
+    explicit HostPool(int threads);
+    ~HostPool();
+    int size() const { return (int)workers_.size() + 1; }
+    void run(int tasks, const std::function<void(int)>& f);
+
+  private:
+    void loop();
+    std::vector<std::thread> workers_;
+    std::mutex m_;
+    std::condition_variable cv_, done_;
+    const std::function<void(int)>* job_ = nullptr;
+    int tasks_ = 0, next_ = 0, active_ = 0;
+    unsigned gen_ = 0;
+    bool stop_ = false;
+};
+}  // namespace bicos_impl
 
 struct bicos_engine {
     int device = 0;
@@ -22,12 +49,21 @@ struct bicos_engine {
     hipStream_t own_stream = nullptr;  // used by the host-buffer APIs
     std::mutex lock;                   // serialises host-buffer calls on this engine
 
-    // workspace (grown on demand, never shrunk)
+    // workspace (grown on demand, never shrunk). ws_ready is recorded after every use of
+    // ws / stage on the caller's stream and waited on before the next: calls on different
+    // streams are ordered, never racing on the shared buffers.
+    hipEvent_t ws_ready = nullptr;
     void* ws = nullptr;
     size_t ws_bytes = 0;
-    // host-API staging
+    // host-API staging (device): band-major stacks + dense output maps
     void* stage = nullptr;
     size_t stage_bytes = 0;
+    // host-buffer pipeline (match_host): copy stream, pinned band slots, band events
+    hipStream_t copy_stream = nullptr;
+    void* pinned = nullptr;  // K input band slots
+    size_t pinned_bytes = 0;
+    std::vector<hipEvent_t> events;
+    std::unique_ptr<bicos_impl::HostPool> pool;
 };
 
 namespace bicos_impl {
@@ -54,7 +90,18 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
                  size_t row_pitch, size_t plane_pitch, int depth, const BicosConfig& cfg,
                  bool has_nxcorr, float threshold, void* disp, void* corr, hipStream_t st);
 
+// Host buffers in and out (the reference's cv::Mat path, src/impl/cpu.cpp:100-159): the
+// stacks are uploaded in row bands through pinned slots on a copy stream while earlier
+// bands match on the compute stream; the maps are downloaded into `disp` / `corr` (dense
+// rows x cols). p0/p1: n plane pointers each, steps0/steps1: bytes per row of each plane.
+// Synchronous.
+int match_host(bicos_engine* e, const void* const* p0, const size_t* steps0,
+               const void* const* p1, const size_t* steps1, int n, int rows, int cols,
+               int depth, const BicosConfig& cfg, bool has_nxcorr, float threshold, void* disp,
+               void* corr);
+
 // Process-wide engine for `device` (created on first use).
 bicos_engine* default_engine(int device);
+bool is_default_engine(const bicos_engine* e);
 
 }  // namespace bicos_impl

@@ -73,19 +73,27 @@ def _stream(device: torch.device, stream=None) -> int:
 class Engine:
     """One bicos_engine (workspace + stream-agnostic launcher) per device."""
 
-    def __init__(self, device=None):
+    def __init__(self, device=None, shared: bool = False):
+        """shared=True wraps the library's process-wide engine for the device (the one
+        BICOS_Match / pybicos.match use) instead of creating a private one."""
         if not torch.cuda.is_available():
             raise RuntimeError("libbicos_amd device engine needs a ROCm GPU")
         self.device = torch.device("cuda", torch.cuda.current_device() if device is None
                                    else torch.device(device).index or 0)
         self._L = _lib.lib()
-        h = ctypes.c_void_p()
-        _lib.check(self._L.bicos_engine_create(self.device.index, ctypes.byref(h)),
-                   "bicos_engine_create")
+        self._owned = not shared
+        if shared:
+            h = ctypes.c_void_p(self._L.bicos_engine_default(self.device.index))
+            if not h.value:
+                _lib.check(-5, "bicos_engine_default")
+        else:
+            h = ctypes.c_void_p()
+            _lib.check(self._L.bicos_engine_create(self.device.index, ctypes.byref(h)),
+                       "bicos_engine_create")
         self._h = h
 
     def close(self):
-        if getattr(self, "_h", None):
+        if getattr(self, "_h", None) and self._owned:
             torch.cuda.synchronize(self.device)
             self._L.bicos_engine_destroy(self._h)
             self._h = None
@@ -193,7 +201,7 @@ _ENGINES = {}
 def default_engine(device=None) -> Engine:
     idx = torch.cuda.current_device() if device is None else torch.device(device).index or 0
     if idx not in _ENGINES:
-        _ENGINES[idx] = Engine(idx)
+        _ENGINES[idx] = Engine(idx, shared=True)
     return _ENGINES[idx]
 
 

@@ -171,7 +171,13 @@ def _marshal(stack):
 
 
 def match(stack0, stack1, cfg=None):
-    """reference pybicos/__init__.py:199-244 -> (disparity, corrmap)."""
+    """reference pybicos/__init__.py:199-244 -> (disparity, corrmap).
+
+    Same inputs, outputs, dtypes and errors as the reference wrapper (which goes through
+    BICOS_Match: NXC always on, so float32 disparity; corrmap float32, or float64 with
+    Precision.DOUBLE). Runs bicos_match_host, which writes the maps straight into the
+    returned arrays (no result struct, no extra copies) and overlaps the upload of the
+    stacks with the match (include/bicos_c.h)."""
     if stack0 is None or stack1 is None or len(stack0) == 0 or len(stack1) == 0:
         raise ValueError("Empty image stacks")
     if cfg is None:
@@ -179,30 +185,21 @@ def match(stack0, stack1, cfg=None):
     L = _lib.lib()
     d0, r0, c0, t0, k0 = _marshal(stack0)
     d1, r1, c1, t1, k1 = _marshal(stack1)
-    result = L.BICOS_Match(d0, r0, c0, t0, len(stack0), d1, r1, c1, t1, len(stack1),
-                           cfg._c_config)
+    f = k0[0]
+    if len(k0) != len(k1) or any(a.shape != f.shape or a.dtype != f.dtype for a in k0 + k1):
+        raise RuntimeError("BICOS matching failed: all images must share size and type "
+                           "(and both stacks the same length)")
+    rows, cols = f.shape
+    ddtype = _get_np_dtype(L.bicos_output_type(cfg._c_config, 1))
+    cdtype = np.float64 if cfg._c_config.contents.precision else np.float32
+    disparity = np.empty((rows, cols), ddtype)
+    corrmap = np.empty((rows, cols), cdtype)
+    rc = L.bicos_match_host(None, d0, d1, len(k0), rows, cols, 0, f.dtype.itemsize,
+                            cfg._c_config, 1, disparity.ctypes.data, corrmap.ctypes.data)
     del k0, k1
-    if not result:
+    if rc != 0:
         raise RuntimeError("BICOS matching failed: " + L.bicos_last_error().decode(errors="replace"))
-    try:
-        res = result.contents
-        dshape = (res.disparity_rows, res.disparity_cols)
-        ddtype = _get_np_dtype(res.disparity_type)
-        disparity = _copy(res.disparity_data, dshape, ddtype)
-        cshape = (res.corrmap_rows, res.corrmap_cols)
-        cdtype = _get_np_dtype(res.corrmap_type)
-        corrmap = _copy(res.corrmap_data, cshape, cdtype)
-    finally:
-        L.BICOS_FreeResult(result)
     return disparity, corrmap
-
-
-def _copy(ptr, shape, dtype):
-    size = shape[0] * shape[1] * np.dtype(dtype).itemsize
-    if size == 0:
-        return np.empty(shape, dtype)
-    buf = (ctypes.c_byte * size).from_address(ptr)
-    return np.frombuffer(buf, dtype=dtype).reshape(shape).copy()
 
 
 def invalid_disparity(dtype):

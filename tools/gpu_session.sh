@@ -34,6 +34,13 @@ for step in "$@"; do
             cp build/cur.so libbicos_amd/libbicos_amd.so ;;
         subpix) run subpix 300 python tools/subpix_bench.py ;;
         subpixs) run subpixs 300 python tools/subpix_bench.py --ns 16,33 --steps 0.5,0.2,0.1,0.05 ;;
+        host) run host 400 python tools/host_bench.py ;;
+        host2) run host2 400 python tools/host_bench.py --reps 9 ;;
+        hosttrace) BICOS_HOST_TRACE=1 run hosttrace 400 python tools/host_bench.py --reps 2 ;;
+        hostknobs)
+            for th in ${HOST_THREADS:-4 8 16}; do
+                BICOS_HOST_THREADS=$th run hostk_${th} 300 python tools/host_bench.py --reps 7
+            done ;;
         subpix16) run subpix16 300 python tools/subpix_bench.py --depth 2 --ns 8,16,24,33 ;;
         bench4) run bench4 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline ;;
         bench5) run bench5 600 python bench.py --config cfg5 --steps 10 --warmup 2 --no-cpu-baseline ;;
