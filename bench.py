@@ -59,26 +59,36 @@ CONFIGS = {
 
 
 def search_pairs(rows: int, W: int, cfg: dict) -> float:
-    """Hamming pairs the search evaluates per match: every (col0, col1) of every row,
-    once per direction (twice with Consistency)."""
-    return float(rows) * W * W * (2 if cfg.get("variant", 0) == 1 else 1)
+    """Hamming pairs per match: every (col0, col1) of every row, i.e. the cost matrix. With
+    Consistency the reference searches it twice (forward, then reverse from each best
+    col1); the fused kernel evaluates each entry once and takes row and column minima, so
+    the algorithmic count stays rows * W^2."""
+    return float(rows) * W * W
 
 
 def search_pair_peak(words: int, cfg: dict) -> float:
-    """Issue-rate bound in pairs/s of the packed search loop's per-pair instruction mix at
-    the measured VALU rates: `words` v_xor (full rate) + `words` v_bcnt (half rate) + half
-    a v_perm and half a v_pk_min_u16 (2 col0 share one packed key register) + with
-    duplicate detection another half v_xor (full) and half v_pk_min_u16 (half rate)."""
-    dupes = cfg.get("variant", 0) == 0 or cfg.get("no_dupes", False)
+    """Issue-rate bound in pairs/s of the search kernel's per-pair instruction mix at the
+    measured VALU rates. Forward (search16_kernel): `words` v_xor (full rate) + `words`
+    v_bcnt (half rate) + half a v_perm and half a v_pk_min_u16 (2 col0 share one packed
+    key register) + with duplicate detection another half v_xor (full) and half
+    v_pk_min_u16 (half). Consistency (search_lr_kernel, 4 col0 per lane) adds the column
+    minima: 1 v_lshl_or + 1/2 v_min3 per pair and per col1 a 6-step DPP v_min reduction
+    (6/4 half-rate per pair) + ~3 full-rate ops (3/4 per pair); all doubled with NoDuplicates."""
+    consistency = cfg.get("variant", 0) == 1
+    dupes = not consistency or cfg.get("no_dupes", False)
     full = words + (0.5 if dupes else 0.0)
     half = words + 1.0 + (0.5 if dupes else 0.0)
+    if consistency:
+        k = 2.0 if dupes else 1.0
+        full += 0.75 * k
+        half += (1.0 + 0.5 + 1.5) * k
     per_pair_s = full / (VALU_FULL_TOPS * 1e12) + half / (VALU_HALF_TOPS * 1e12)
     return 1.0 / per_pair_s
 
 
 def search_ops(rows: int, W: int, words: int, cfg: dict) -> float:
-    """Reference-algorithm INT32 lane-ops (32-bit keys): per pair `words` xor + `words`
-    bcnt + key pack + min (+ med3 with NoDuplicates) = 2w+3 (2w+2 without)."""
+    """INT32 lane-ops of one pass over the cost matrix with 32-bit keys: per pair `words`
+    xor + `words` bcnt + key pack + min (+ med3 with NoDuplicates) = 2w+3 (2w+2 without)."""
     dupes = cfg.get("variant", 0) == 0 or cfg.get("no_dupes", False)
     return search_pairs(rows, W, cfg) * (2 * words + (3 if dupes else 2))
 
@@ -271,7 +281,9 @@ def main():
     traffic = load_traffic("search16_kernel", rows, W) if args.config == "cfg2" and rows == H else None
 
     roof = {
-        "kernel": "search16_kernel<%d words> (Hamming argmin, packed 16-bit keys)" % words,
+        "kernel": ("search_lr_kernel<%d words> (fused forward + reverse Hamming argmin)" % words
+                   if C["cfg"].get("variant", 0) == 1 else
+                   "search16_kernel<%d words> (Hamming argmin, packed 16-bit keys)" % words),
         "bound": "valu",
         "achieved": round(achieved, 1),
         "peak": round(peak, 1),
@@ -288,7 +300,7 @@ def main():
         "lane_ops_view": {
             "achieved_Tops": round(search_ops(rows, W, words, C["cfg"]) / t_search / 1e12, 2),
             "nominal_peak_Tops": round(VALU_NOMINAL_TOPS, 1),
-            "ops_model": "reference algorithm, 32-bit keys: 2w+3 lane-ops per pair",
+            "ops_model": "one pass over the cost matrix, 32-bit keys: 2w+3 (2w+2) lane-ops per pair",
         },
         "hbm": {
             "transform_GBps": round(tf_bytes / t_tf / 1e9, 1),

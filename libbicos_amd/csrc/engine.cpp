@@ -85,6 +85,30 @@ bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, in
                                       e->tune_waves, e->tune_split, e->cus);
 }
 
+bool fused_consistency() {
+    // one fused forward+reverse search (search_lr_kernel) unless BICOS_CONSISTENCY=twopass
+    // asks for a forward and a full reverse search (A/B; identical results)
+    static const bool twopass = [] {
+        const char* v = std::getenv("BICOS_CONSISTENCY");
+        return v && !std::strcmp(v, "twopass");
+    }();
+    return !twopass;
+}
+
+bicos_hip::SearchGeometry geometry_lr(const bicos_engine* e, int rows, int cols, int words,
+                                      bool nodupes) {
+    // row stage + one (two with NoDuplicates) 32-bit column key per col1; up to 80 KiB so a
+    // 256-bit 2048-column row stays one stage with 2 workgroups per CU (160 KiB LDS)
+    const int limit = e ? e->lds_limit : 64 * 1024;
+    const int budget = limit < 80 * 1024 ? limit : 80 * 1024;
+    const int extra = 4 * (nodupes ? 2 : 1);
+    if (!e) return bicos_hip::search_geometry(rows, cols, words, budget, 16, 4, 0, 0, 256, extra);
+    // 4 col0 per lane by default: the per-col1 wave reduction amortises over more pairs
+    const int R = (e->tune_R == 2 || e->tune_R == 4) ? e->tune_R : 4;
+    return bicos_hip::search_geometry(rows, cols, words, budget, 16, R, e->tune_waves,
+                                      e->tune_split, e->cus, extra);
+}
+
 // Number of x the reference's subpixel loop visits: for (float x = -1.f; x <= 1.f; x += step)
 // (agree.hpp:122 / agree.cuh:213), accumulated in float exactly as there. 0 when the loop
 // would exceed MAX_SUBPIXEL_STEPS (or never end: x + step == x), which the reference would
@@ -148,11 +172,17 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     const bool nodupes = consistency ? cfg.no_dupes != 0 : true;
     const bool dbl = cfg.precision != 0;
 
-    // workspace: desc0 | desc1 | raw int16 | fwd | rev
+    const bool fused = consistency && fused_consistency();
+    const bicos_hip::SearchGeometry glr =
+        fused ? geometry_lr(e, rows, cols, words, nodupes) : bicos_hip::SearchGeometry{};
+
+    // workspace: desc0 | desc1 | raw int16 | fwd | rev (two-pass) or rev keys (fused)
     const size_t dpitch = bicos_desc_pitch(cols, words);
     const size_t desc_bytes = align_up((size_t)rows * dpitch * 4);
     const size_t map16 = align_up((size_t)rows * cols * 2);
-    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) + (consistency ? 2 * map16 : 0);
+    const size_t keys = fused ? align_up((size_t)rows * glr.tiles_per_row * cols * 4) : 0;
+    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) +
+                  (consistency ? (fused ? map16 + keys * (nodupes ? 2 : 1) : 2 * map16) : 0);
     int rc = reserve(e->ws, e->ws_bytes, need, e->device);
     if (rc) return rc;
     // order against earlier users of ws / stage on other streams; mark our use on exit
@@ -171,7 +201,9 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     int16_t* raw = has_nxcorr ? (int16_t*)p : (int16_t*)disp;
     if (has_nxcorr) p += map16;
     int16_t* fwd = consistency ? (int16_t*)p : nullptr;
-    int16_t* rev = consistency ? (int16_t*)(p + map16) : nullptr;
+    int16_t* rev = consistency && !fused ? (int16_t*)(p + map16) : nullptr;
+    uint32_t* rev_first = fused ? (uint32_t*)(p + map16) : nullptr;
+    uint32_t* rev_last = fused && nodupes ? (uint32_t*)(p + map16 + keys) : nullptr;
 
     // 1. descriptor_transform, both stacks in one launch (cpu.cpp:50-59)
     bicos_hip::TransformArgs ta{s0, s1, d0, d1, n, rows, cols, row_pitch, plane_pitch, dpitch, 0, span};
@@ -183,6 +215,19 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     if (!consistency) {
         bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
         rc = check_hip(bicos_hip::launch_search(sa, g, words, true, st), "search launch");
+        if (rc) return rc;
+    } else if (fused) {
+        bicos_hip::SearchArgs fa{d0, d1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
+        fa.rev_first = rev_first;
+        fa.rev_last = rev_last;
+        rc = check_hip(bicos_hip::launch_search_lr(fa, glr, words, nodupes, st),
+                       "fused consistency search launch");
+        if (rc) return rc;
+        bicos_hip::ConsistencyArgs ca{fwd, nullptr, raw, rows, cols, (size_t)cols, cfg.max_lr_diff};
+        ca.rev_first = rev_first;
+        ca.rev_last = rev_last;
+        ca.rev_tiles = glr.tiles_per_row;
+        rc = check_hip(bicos_hip::launch_consistency_keys(ca, st), "consistency launch");
         if (rc) return rc;
     } else {
         bicos_hip::SearchArgs fa{d0, d1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
@@ -484,6 +529,7 @@ int bicos_engine_create(int device, bicos_engine** out) {
         lds > 0) {
         // keep the per-workgroup right-row stage <= 64 KiB so >= 2 workgroups fit per CU
         e->max_lds = lds < 64 * 1024 ? lds : 64 * 1024;
+        e->lds_limit = lds;
     }
     int cus = 0;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) == hipSuccess &&
@@ -642,6 +688,31 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     }
     if (!e) return fail(BICOS_E_ARG, "consistency search needs an engine workspace");
     const size_t map16 = align_up((size_t)rows * cols * 2);
+    if (fused_consistency()) {
+        const bicos_hip::SearchGeometry glr = geometry_lr(e, rows, cols, words, nodupes);
+        const size_t keys = align_up((size_t)rows * glr.tiles_per_row * cols * 4);
+        int rc = reserve(e->ws, e->ws_bytes, map16 + keys * (nodupes ? 2 : 1), e->device);
+        if (rc) return rc;
+        rc = check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent");
+        if (rc) return rc;
+        int16_t* fwd = (int16_t*)e->ws;
+        uint32_t* rev_first = (uint32_t*)((char*)e->ws + map16);
+        uint32_t* rev_last = nodupes ? (uint32_t*)((char*)e->ws + map16 + keys) : nullptr;
+        bicos_hip::SearchArgs fa{desc0, desc1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
+        fa.rev_first = rev_first;
+        fa.rev_last = rev_last;
+        rc = check_hip(bicos_hip::launch_search_lr(fa, glr, words, nodupes, st),
+                       "fused consistency search launch");
+        if (!rc) {
+            bicos_hip::ConsistencyArgs ca{fwd, nullptr, out, rows, cols, (size_t)cols, max_lr_diff};
+            ca.rev_first = rev_first;
+            ca.rev_last = rev_last;
+            ca.rev_tiles = glr.tiles_per_row;
+            rc = check_hip(bicos_hip::launch_consistency_keys(ca, st), "consistency launch");
+        }
+        (void)hipEventRecord(e->ws_ready, st);
+        return rc;
+    }
     int rc = reserve(e->ws, e->ws_bytes, 2 * map16, e->device);
     if (rc) return rc;
     int16_t* fwd = (int16_t*)e->ws;

@@ -42,7 +42,8 @@ class HostPool {
 
 struct bicos_engine {
     int device = 0;
-    int max_lds = 64 * 1024;
+    int max_lds = 64 * 1024;           // search row stage budget (>= 2 workgroups per CU)
+    int lds_limit = 64 * 1024;         // device limit per workgroup
     int cus = 256;                     // compute units (workgroup geometry)
     // search kernel tuning (0 = automatic): see bicos_engine_tune
     int tune_variant = 0, tune_R = 0, tune_waves = 0, tune_split = 0;
@@ -84,6 +85,11 @@ int reserve(void*& buf, size_t& have, size_t bytes, int device);
 int descriptor_words(int n, int mode);
 
 bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, int words);
+// Consistency runs the fused search unless BICOS_CONSISTENCY=twopass
+bool fused_consistency();
+// geometry of the fused Consistency search (row stage + per-column keys in LDS)
+bicos_hip::SearchGeometry geometry_lr(const bicos_engine* e, int rows, int cols, int words,
+                                      bool nodupes);
 
 // Full match on device buffers (validated arguments). corr may be null.
 int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int rows, int cols,

@@ -32,6 +32,9 @@ struct SearchArgs {
     int chunk;              // set by launch_search
     int tiles_per_row;      // set by launch_search
     int split;              // set by launch_search: waves per col0 group scanning col1 tiles
+    // fused Consistency (launch_search_lr): per-tile column minima [rows][tiles][cols]
+    uint32_t* rev_first = nullptr;
+    uint32_t* rev_last = nullptr;  // NoDuplicates only
 };
 
 struct SearchGeometry {
@@ -50,6 +53,10 @@ struct ConsistencyArgs {
     int rows, cols;
     size_t out_pitch;
     int max_lr_diff;
+    // fused search (consistency_keys_kernel): per-tile column minima instead of `rev`
+    const uint32_t* rev_first = nullptr;
+    const uint32_t* rev_last = nullptr;
+    int rev_tiles = 0;
 };
 
 struct AgreeArgs {
@@ -72,10 +79,17 @@ struct AgreeArgs {
 
 hipError_t launch_transform(TransformArgs a, int depth, int mode, int words, hipStream_t st);
 SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes, int variant = 16,
-                               int R = 0, int waves = 0, int split = 0, int cus = 256);
+                               int R = 0, int waves = 0, int split = 0, int cus = 256,
+                               int extra_col_bytes = 0);
 hipError_t launch_search(SearchArgs a, const SearchGeometry& g, int words, bool nodupes,
                          hipStream_t st);
 hipError_t launch_consistency(const ConsistencyArgs& a, hipStream_t st);
+// Fused forward + reverse search (Consistency): a.out gets the forward best col1 (or -1),
+// a.rev_first / a.rev_last [rows][g.tiles_per_row][cols] the column minima; g from
+// search_geometry(..., extra_col_bytes = 4 * (1 + nodupes)).
+hipError_t launch_search_lr(SearchArgs a, const SearchGeometry& g, int words, bool nodupes,
+                            hipStream_t st);
+hipError_t launch_consistency_keys(const ConsistencyArgs& a, hipStream_t st);
 hipError_t launch_agree(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
 hipError_t launch_subpixel(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
 

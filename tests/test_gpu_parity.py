@@ -281,6 +281,29 @@ def test_empty_and_tiny(gpu, oracle):
         same(gpu_match(gpu, L, R, **cfg)[0], oracle.match(L, R, cfg_of(oracle, **cfg))[0])
 
 
+# Fused forward + reverse Consistency search (search_lr_kernel): rows wider than one LDS
+# stage (column minima flushed per stage), reverse duplicates (low-entropy stacks), every
+# register blocking / col1 split, and several col0 tiles per row.
+@pytest.mark.parametrize("n,H,W,maxval", [(40, 3, 2600, None), (17, 5, 3000, None),
+                                          (8, 6, 700, 3), (33, 4, 1100, 2)])
+@pytest.mark.parametrize("no_dupes", [False, True])
+def test_fused_consistency_edges(gpu, oracle, n, H, W, maxval, no_dupes):
+    if maxval is None:
+        L, R = stereo_stack(n, H, W, dmin=4, drange=40, seed=n + W)
+    else:
+        L = random_stack(n, H, W, seed=n, maxval=maxval)
+        R = random_stack(n, H, W, seed=n + 1, maxval=maxval)
+    kw = dict(nxcorr_threshold=None, variant=1, max_lr_diff=2, no_dupes=no_dupes)
+    rd, _ = oracle.match(L, R, cfg_of(oracle, **kw))
+    for R_, split in [(0, 0), (2, 0), (4, 2), (2, 4), (4, 8)]:
+        gpu.tune(16, R_, 8, split)
+        try:
+            d, _ = gpu_match(gpu, L, R, **kw)
+        finally:
+            gpu.tune(0, 0, 0, 0)
+        same(d, rd)
+
+
 def test_errors(gpu):
     import torch
     from libbicos_amd import BicosError

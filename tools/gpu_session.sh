@@ -21,7 +21,7 @@ for step in "$@"; do
         pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
         pytestk) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
         bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
-        bench3) run bench3 600 python bench.py --config cfg3 --steps 10 --warmup 2 --no-cpu-baseline ;;
+        bench3) run bench3 600 python bench.py --config cfg3 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
         ab3|ab2|ab4)  # A/B on one box: current lib vs build/alt.so (same bench, interleaved twice)
             c=cfg${step#ab}
             cp libbicos_amd/libbicos_amd.so build/cur.so
@@ -42,7 +42,9 @@ for step in "$@"; do
                 BICOS_HOST_THREADS=$th run hostk_${th} 300 python tools/host_bench.py --reps 7
             done ;;
         subpix16) run subpix16 300 python tools/subpix_bench.py --depth 2 --ns 8,16,24,33 ;;
-        bench4) run bench4 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline ;;
+        bench4) run bench4 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
+        bench4tp) BICOS_CONSISTENCY=twopass run bench4tp 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
+        pytesttp) BICOS_CONSISTENCY=twopass run pytest_tp 900 python -m pytest tests -m gpu -x -q -k "consist or cons or cfg4 or golden or tuning" ;;
         bench5) run bench5 600 python bench.py --config cfg5 --steps 10 --warmup 2 --no-cpu-baseline ;;
         sweep) run sweep 600 python tools/search_sweep.py --variants 16:2:8:2,18:2:8:2,16:2:8:1,18:2:8:1,18:4:8:2,17:2:8:2 ;;
         sweep4) run sweep4 600 python tools/search_sweep.py --config cfg4 --variants 16:2:8:2,18:2:8:2,18:4:8:2 ;;
