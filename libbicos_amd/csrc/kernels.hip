@@ -1093,12 +1093,31 @@ __global__ __launch_bounds__(256) void agree_kernel(AgreeArgs a) {
     if (a.corrmap) ((TPrec*)a.corrmap)[o] = corr;
 }
 
+// (column tile, row) of a (tiles x rows) grid, remapped so that each XCD gets a run of
+// whole rows: workgroups are dispatched round-robin over the 8 XCDs in linear order, so
+// without this neighbouring column tiles land on different XCDs and the right-image
+// windows they share (col - d, col1 +- 1) are fetched into two L2s.
+__device__ __forceinline__ void xcd_rows(int& tile, int& row) {
+    const int gx = gridDim.x;
+    const int nwg = gx * gridDim.y;
+    if (nwg % 8) {
+        tile = blockIdx.x;
+        row = blockIdx.y;
+        return;
+    }
+    const int bid = blockIdx.y * gx + blockIdx.x;
+    const int logical = (bid % 8) * (nwg / 8) + bid / 8;
+    tile = logical % gx;
+    row = logical / gx;
+}
+
 // agree with the 2n samples loaded once into registers (MAXN >= n), the same arithmetic
 // and output contract as agree_kernel.
 template <typename TIn, typename TPrec, int MAXN, bool EXACT>
 __global__ __launch_bounds__(256) void agree_reg_kernel(AgreeArgs a) {
-    const int col = blockIdx.x * 256 + threadIdx.x;
-    const int row = blockIdx.y;
+    int tile, row;
+    xcd_rows(tile, row);
+    const int col = tile * 256 + threadIdx.x;
     if (col >= a.cols) return;
     const size_t o = (size_t)row * a.cols + col;
     int d = a.raw[(size_t)row * a.raw_pitch + col];
@@ -1188,8 +1207,9 @@ __device__ __forceinline__ float interp_wrapped(float A, float B, float C, float
 // in float exactly as the reference's loop (engine.cpp subpixel_steps).
 template <typename TIn, typename TPrec, int MAXN, int LO>
 __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
-    const int col = blockIdx.x * 256 + threadIdx.x;
-    const int row = blockIdx.y;
+    int tile, row;
+    xcd_rows(tile, row);
+    const int col = tile * 256 + threadIdx.x;
     if (col >= a.cols) return;
     const size_t o = (size_t)row * a.cols + col;
     const int n = LO == MAXN ? MAXN : a.n;

@@ -22,7 +22,7 @@ for step in "$@"; do
         pytestk) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
         bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
         bench3) run bench3 600 python bench.py --config cfg3 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
-        ab3|ab2|ab4)  # A/B on one box: current lib vs build/alt.so (same bench, interleaved twice)
+        ab1|ab3|ab2|ab4)  # A/B on one box: current lib vs build/alt.so (same bench, interleaved twice)
             c=cfg${step#ab}
             cp libbicos_amd/libbicos_amd.so build/cur.so
             for k in 1 2; do
