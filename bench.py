@@ -53,6 +53,9 @@ CONFIGS = {
     "cfg4": dict(n=40, H=1536, W=2048, dtype="u8",
                  cfg=dict(nxcorr_threshold=0.96, variant=1, max_lr_diff=1),
                  desc="40x2 @ 2048x1536 u8, LIMITED 256-bit, LR-consistency max_lr_diff 1, nxcorr 0.96"),
+    "cfg4f": dict(n=40, H=1536, W=2048, dtype="u8", cfg=dict(nxcorr_threshold=0.96),
+                  desc="40x2 @ 2048x1536 u8, LIMITED 256-bit, NoDuplicates, nxcorr 0.96 (cfg4 "
+                       "without Consistency; not a BASELINE config)"),
     "cfg5": dict(n=33, H=2160, W=3840, dtype="u8", cfg=dict(nxcorr_threshold=0.96),
                  desc="33x2 @ 3840x2160 u8, 128-bit, nxcorr 0.96"),
 }

@@ -79,7 +79,24 @@ int descriptor_words(int n, int mode) {
 }
 
 bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, int words) {
-    const int max_lds = e ? e->max_lds : 64 * 1024;
+    int max_lds = e ? e->max_lds : 64 * 1024;
+    // Row stage budget per workgroup (BICOS_SEARCH_STAGE_KIB, default 40; 0 = whole rows up
+    // to 64 KiB): wider rows are split into equal chunks under it, so 4 workgroups (8 waves
+    // per SIMD) stay resident per CU. Measured: 3840-column rows (cfg5) search -2.6 %,
+    // 256-bit 2048-column rows -1.3 %; rows that fit (cfg2: 32 KiB) are unchanged.
+    static const int stage_kib = [] {
+        const char* v = std::getenv("BICOS_SEARCH_STAGE_KIB");
+        return v ? std::atoi(v) : 40;
+    }();
+    if (stage_kib > 0) {
+        const int budget = stage_kib * 1024;
+        const int bytes = cols * words * 4;
+        if (bytes > budget) {
+            const int chunks = (bytes + budget - 1) / budget;
+            const int chunk = (cols + chunks - 1) / chunks;
+            max_lds = std::min(max_lds, chunk * words * 4);
+        }
+    }
     if (!e) return bicos_hip::search_geometry(rows, cols, words, max_lds);
     return bicos_hip::search_geometry(rows, cols, words, max_lds, e->tune_variant, e->tune_R,
                                       e->tune_waves, e->tune_split, e->cus);

@@ -659,6 +659,7 @@ __global__ __launch_bounds__(512) void search16_kernel(SearchArgs a) {
     const int lane = threadIdx.x % 64;
     const int cols = a.cols;
     const int col0_base = tile * groups * 64 * R + group * 64 * R + lane;
+    const bool idle = col0_base - lane >= cols;  // wave-uniform
     const uint32_t top_mask = WORDS == 8 ? 0x7FFFFFFFu : 0xFFFFFFFFu;
 
     const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
@@ -692,7 +693,9 @@ __global__ __launch_bounds__(512) void search16_kernel(SearchArgs a) {
         }
         __syncthreads();
 
-        for (int t0 = seg * 256; t0 < ncols; t0 += 256 * split) {
+        // a wave whose col0 all lie beyond the image (last tile of a row) has nothing to
+        // search: it only helps stage the row (cfg5, 3840 columns: 6 % of the waves)
+        for (int t0 = idle ? ncols : seg * 256; t0 < ncols; t0 += 256 * split) {
             const int tn = min(256, ncols - t0);
             uint32_t lo[RP], hi[RP];
 #pragma unroll
@@ -818,6 +821,7 @@ __global__ __launch_bounds__(512) void search_lr_kernel(SearchArgs a) {
     const int cols = a.cols;
     const int grp_base = tile * groups * 64 * R + group * 64 * R;
     const int col0_base = grp_base + lane;
+    const bool idle = grp_base >= cols;  // no col0 of this wave in the image: stage only
     const uint32_t top_mask = WORDS == 8 ? 0x7FFFFFFFu : 0xFFFFFFFFu;
 
     const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
@@ -859,7 +863,7 @@ __global__ __launch_bounds__(512) void search_lr_kernel(SearchArgs a) {
         }
         __syncthreads();
 
-        for (int t0 = seg * 256; t0 < ncols; t0 += 256 * split) {
+        for (int t0 = idle ? ncols : seg * 256; t0 < ncols; t0 += 256 * split) {
             const int tn = min(256, ncols - t0);
             uint32_t lo[RP], hi[RP];
 #pragma unroll

@@ -45,14 +45,18 @@ for step in "$@"; do
         bench4) run bench4 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
         bench4tp) BICOS_CONSISTENCY=twopass run bench4tp 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
         pytesttp) BICOS_CONSISTENCY=twopass run pytest_tp 900 python -m pytest tests -m gpu -x -q -k "consist or cons or cfg4 or golden or tuning" ;;
-        bench5) run bench5 600 python bench.py --config cfg5 --steps 10 --warmup 2 --no-cpu-baseline ;;
+        stagekib)
+            for c in cfg5 cfg4f; do for k in 0 40 32; do
+                BICOS_SEARCH_STAGE_KIB=$k run stage_${c}_$k 300 python bench.py --config $c --steps 8 --warmup 2 --no-cpu-baseline --no-host-path
+            done; done ;;
+        bench5) run bench5 600 python bench.py --config cfg5 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
         sweep) run sweep 600 python tools/search_sweep.py --variants 16:2:8:2,18:2:8:2,16:2:8:1,18:2:8:1,18:4:8:2,17:2:8:2 ;;
         sweep4) run sweep4 600 python tools/search_sweep.py --config cfg4 --variants 16:2:8:2,18:2:8:2,18:4:8:2 ;;
         sweep1) run sweep1 600 python tools/search_sweep.py --config cfg1 --variants 32:1:4,32:2:4,16:2:4,16:4:4,16:2:2,16:2:1 ;;
         sweep8) run sweep8 600 python tools/search_sweep.py --rows 192 --variants 0:0:0:0,16:2:8:4,16:2:8:8,16:4:8:8 ;;
         sweep48) run sweep48 600 python tools/search_sweep.py --rows 384 --variants 0:0:0:0,16:2:8:2,16:2:8:4,16:2:8:8 && python tools/search_sweep.py --rows 768 --variants 0:0:0:0,16:2:8:1,16:2:8:2,16:2:8:4 && python tools/search_sweep.py --config cfg5 --rows 270 --variants 0:0:0:0,16:2:8:4,16:2:8:8 ;;
         sweep5) run sweep5 600 python tools/search_sweep.py --config cfg5 --rows 270 --variants 0:0:0:0,16:2:8:1,16:2:8:2,16:2:8:4 ;;
-        rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --steps 5 --warmup 1 --no-cpu-baseline ;;
+        rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --steps 5 --warmup 1 --no-cpu-baseline --no-host-path ;;
         pmcsub) run pmcsub 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmcsub -o run --output-format csv -- python bench.py --config cfg3 --steps 2 --warmup 1 --no-cpu-baseline --kernel-reps 1 ;;
         prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
         pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 2 ;;
