@@ -159,6 +159,24 @@ def test_subpixel_bit_exact(gpu, oracle, n, dt, step, minvar):
     same(host(corr), rc)
 
 
+# Narrow images and every col1 (0, 1, interior, cols-2, cols-1): the subpixel kernel reads
+# the right neighbours with one window load except below 4 columns (byte loads).
+@pytest.mark.parametrize("W", [3, 4, 5, 9])
+@pytest.mark.parametrize("n,dt", [(8, np.uint8), (17, np.uint16), (33, np.uint8)])
+def test_subpixel_narrow_images_every_col1(gpu, oracle, W, n, dt):
+    H = 6
+    L = random_stack(n, H, W, dt, seed=W + n)
+    R = random_stack(n, H, W, dt, seed=W + n + 1)
+    raw = np.empty((H, W), np.int16)
+    for y in range(H):
+        for x in range(W):
+            raw[y, x] = x - ((x + y) % W)  # col1 = (x + y) % W: all columns appear
+    ro, rc = oracle.agree_subpixel(raw, L, R, 0.1, 0.25, None)
+    out, corr = gpu.agree(dev(raw), dev(L), dev(R), 0.1, None, step=0.25)
+    same(host(out), ro)
+    same(host(corr), rc)
+
+
 # -------------------------------------------------------------- full match
 CFGS = [
     dict(nxcorr_threshold=None),
