@@ -119,6 +119,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--spinup-ms", type=float, default=100.0,
+                    help="untimed warm-up lasts at least this long (GPU clock ramp), >= W steps")
     ap.add_argument("--config", default="cfg2", choices=sorted(CONFIGS))
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="strong: one frame split in row bands; weak: a full frame per GPU")
@@ -217,10 +219,24 @@ def main():
                     pending[i].wait()
                     pending[i] = None
 
+    # Untimed warm-up. First a clock spin-up: at least --spinup-ms of back-to-back local
+    # matches (no collectives, so ranks need not agree on a count). The GPU's clocks ramp
+    # for ~25 ms under this load (rocprof trace in profiles/: the search kernel goes from
+    # 1.78 to 1.56 ms over its first 13 launches), and K timed steps right after 3 warm-up
+    # matches would average part of that ramp into a steady-state frame rate. Then the W
+    # regular warm-up steps (with the gather), identical on every rank.
+    t_warm = time.perf_counter()
+    spins = 0
+    while (time.perf_counter() - t_warm) * 1e3 < args.spinup_ms:
+        for _ in range(4):
+            eng.match(s0, s1, mcfg, out=out, corrmap=corr)
+        spins += 4
+        torch.cuda.synchronize(dev)
     for _ in range(args.warmup):
         step()
     drain()
     torch.cuda.synchronize(dev)
+    warm_ms = (time.perf_counter() - t_warm) * 1e3
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
@@ -333,6 +349,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "spinup_matches": spins,
+            "warmup_ms": round(warm_ms, 1),
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
             "scaling": args.scaling,

@@ -58,11 +58,11 @@ for step in "$@"; do
         sweep5) run sweep5 600 python tools/search_sweep.py --config cfg5 --rows 270 --variants 0:0:0:0,16:2:8:1,16:2:8:2,16:2:8:4 ;;
         rehearse2) run rehearse2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --backend gloo --steps 5 --warmup 1 --no-cpu-baseline --no-host-path ;;
         pmcsub) run pmcsub 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE -d gpurun_out/pmcsub -o run --output-format csv -- python bench.py --config cfg3 --steps 2 --warmup 1 --no-cpu-baseline --kernel-reps 1 ;;
-        prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
-        pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 2 ;;
-        pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 2 ;;
-        pmcs) run pmcs 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d gpurun_out/pmcs -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 2 ;;
-        pmcl) run pmcl 600 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_INSTS_VALU_INT32 TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmcl -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --kernel-reps 2 ;;
+        prof) run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
+        pmcf) run pmcf 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmcf -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-path --kernel-reps 2 ;;
+        pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-path --kernel-reps 2 ;;
+        pmcs) run pmcs 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d gpurun_out/pmcs -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-path --kernel-reps 2 ;;
+        pmcl) run pmcl 600 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_INSTS_VALU_INT32 TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmcl -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-path --kernel-reps 2 ;;
         *) echo "unknown step $step" ;;
     esac
 done
