@@ -264,20 +264,36 @@ def main():
     raw = torch.empty((rows, W), dtype=torch.int16, device=dev)
     flags = (2 | (1 if mcfg.no_dupes else 0)) if mcfg.variant == 1 else 1
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-    eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw)  # warm
+    # the pipeline fuses the NXC agree into the search epilogue when there is no
+    # Consistency / subpixel / DOUBLE (engine.cpp match_device): time that launch then
+    mc = C["cfg"]
+    fused_agree = (mcfg.variant == 0 and mcfg.nxcorr_threshold is not None and
+                   not mc.get("subpixel_step") and not mcfg.precision and
+                   os.environ.get("BICOS_FUSE_AGREE", "1") != "0")
+    mv = mc.get("min_variance")
+    mv = None if mv is None or mv < 0 else mv * n
+
+    def search_launch():
+        if fused_agree:
+            eng.search_agree(d0, d1, s0, s1, words, mcfg.nxcorr_threshold, minvar_scaled=mv)
+        else:
+            eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw)
+
+    search_launch()  # warm
     ev[0].record(st)
     for _ in range(args.kernel_reps):
-        eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw)
+        search_launch()
     ev[1].record(st)
     for _ in range(args.kernel_reps):
         eng.transform(s0, mcfg.mode, words, out=d0)
     ev[2].record(st)
+    if fused_agree:  # the standalone agree below needs the int16 search result
+        eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw)
     # the agree stage this config runs: NXC (agree_reg_kernel) or NXC + subpixel refine
-    mc = C["cfg"]
     thr = mc.get("nxcorr_threshold")
-    mv = mc.get("min_variance")
-    mv = None if mv is None or mv < 0 else mv * n
     stage = "subpixel" if mc.get("subpixel_step") else "nxcorr"
+    if fused_agree:
+        stage = "nxcorr (standalone agree_reg_kernel; the pipeline runs it fused in the search)"
     ev[3].record(st)
     for _ in range(args.kernel_reps):
         eng.agree(raw, s0, s1, 0.96 if thr is None else thr, minvar_scaled=mv,
@@ -302,7 +318,8 @@ def main():
     roof = {
         "kernel": ("search_lr_kernel<%d words> (fused forward + reverse Hamming argmin)" % words
                    if C["cfg"].get("variant", 0) == 1 else
-                   "search16_kernel<%d words> (Hamming argmin, packed 16-bit keys)" % words),
+                   "search16_kernel<%d words> (Hamming argmin, packed 16-bit keys)%s" %
+                   (words, " + fused NXC agree epilogue" if fused_agree else "")),
         "bound": "valu",
         "achieved": round(achieved, 1),
         "peak": round(peak, 1),

@@ -229,6 +229,31 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
 
     // 2. bicos search (cpu.cpp:68-75)
     const bicos_hip::SearchGeometry g = geometry(e, rows, cols, words);
+    // NXC agree fused into the search epilogue (no Consistency, no subpixel, single
+    // precision, default search variant) unless BICOS_FUSE_AGREE=0
+    static const bool fuse_env = [] {
+        const char* v = std::getenv("BICOS_FUSE_AGREE");
+        return !(v && !std::strcmp(v, "0"));
+    }();
+    const bool has_step_ = has_nxcorr && cfg.subpixel_step >= 0;
+    const bool fuse_agree = fuse_env && !consistency && has_nxcorr && !has_step_ && !dbl &&
+                            g.variant == 16;
+    if (fuse_agree) {
+        bicos_hip::SearchArgs sa{d0, d1, nullptr, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
+        sa.out_f32 = (float*)disp;
+        sa.corr = (float*)corr;
+        sa.stack0 = s0;
+        sa.stack1 = s1;
+        sa.n = n;
+        sa.depth = depth;
+        sa.row_pitch = row_pitch;
+        sa.plane_pitch = plane_pitch;
+        sa.threshold = threshold;
+        sa.has_minvar = cfg.min_variance >= 0;
+        sa.minvar = sa.has_minvar ? cfg.min_variance * (float)n : 0.f;  // cpu.cpp:127
+        return check_hip(bicos_hip::launch_search(sa, g, words, true, st),
+                         "search + agree launch");
+    }
     if (!consistency) {
         bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
         rc = check_hip(bicos_hip::launch_search(sa, g, words, true, st), "search launch");
@@ -742,6 +767,39 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     if (rc) return rc;
     bicos_hip::ConsistencyArgs ca{fwd, rev, out, rows, cols, (size_t)cols, max_lr_diff};
     return check_hip(bicos_hip::launch_consistency(ca, st), "consistency launch");
+}
+
+int bicos_search_agree_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* desc1,
+                              const void* stack0, const void* stack1, int n, int rows, int cols,
+                              size_t row_pitch, size_t plane_pitch, int depth, int words,
+                              float threshold, int has_minvar, float minvar_scaled, float* out,
+                              float* corrmap, void* stream) {
+    if (words != 1 && words != 2 && words != 4 && words != 8)
+        return fail(BICOS_E_ARG, "words must be 1, 2, 4 or 8");
+    if (n < 2) return fail(BICOS_E_ARG, "need at least two images");
+    if (depth != 1 && depth != 2) return fail(BICOS_E_ARG, "bad input depth");
+    if (cols > 32767) return fail(BICOS_E_ARG, "image width exceeds 32767");
+    if (rows <= 0 || cols <= 0) return BICOS_OK;
+    if (!desc0 || !desc1 || !stack0 || !stack1 || !out) return fail(BICOS_E_ARG, "null buffer");
+    if (row_pitch < (size_t)cols || plane_pitch < (size_t)rows * row_pitch)
+        return fail(BICOS_E_ARG, "row/plane pitch smaller than the image");
+    bicos_hip::SearchGeometry g = geometry(e, rows, cols, words);
+    if (g.variant != 16) g = bicos_hip::search_geometry(rows, cols, words, e ? e->max_lds : 64 * 1024);
+    bicos_hip::SearchArgs sa{desc0, desc1, nullptr, rows, cols, bicos_desc_pitch(cols, words),
+                             (size_t)cols, 0, 0, 0};
+    sa.out_f32 = out;
+    sa.corr = corrmap;
+    sa.stack0 = stack0;
+    sa.stack1 = stack1;
+    sa.n = n;
+    sa.depth = depth;
+    sa.row_pitch = row_pitch;
+    sa.plane_pitch = plane_pitch;
+    sa.threshold = threshold;
+    sa.has_minvar = has_minvar;
+    sa.minvar = minvar_scaled;
+    return check_hip(bicos_hip::launch_search(sa, g, words, true, (hipStream_t)stream),
+                     "search + agree launch");
 }
 
 static int agree_common(bool sub, const int16_t* raw, const void* stack0, const void* stack1,

@@ -20,6 +20,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace bicos_hip {
 
 namespace {
@@ -636,7 +638,13 @@ __device__ __forceinline__ void search16_step(const uint32_t* s, uint32_t seed,
     }
 }
 
-template <int WORDS, bool NODUPES, int RP, int STEP>
+__device__ __forceinline__ float fma_p(float a, float b, float c);
+__device__ __forceinline__ float div_p(float a, float b);
+__device__ __forceinline__ float sqrt_p(float x);
+
+// FUSE: 0 = plain search (int16 `out`), 1 / 2 = fused NXC agree epilogue on u8 / u16
+// stacks (agree.hpp:53-93 for the pixels this workgroup owns; see SearchArgs)
+template <int WORDS, bool NODUPES, int RP, int STEP, int FUSE = 0>
 __global__ __launch_bounds__(512) void search16_kernel(SearchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
 
@@ -758,6 +766,74 @@ __global__ __launch_bounds__(512) void search16_kernel(SearchArgs a) {
             }
     }
 
+    if constexpr (FUSE != 0) {
+        // agree for this lane's pixels: col1 = best is always in the row, so NXC runs for
+        // every non-duplicate pixel; threshold -> float disparity, corrmap NaN otherwise
+        using TIn = typename std::conditional<FUSE == 1, uint8_t, uint16_t>::type;
+        const TIn* s0 = (const TIn*)a.stack0 + (size_t)row * a.row_pitch;
+        const TIn* s1 = (const TIn*)a.stack1 + (size_t)row * a.row_pitch;
+        float* outf = a.out_f32 + (size_t)row * a.out_pitch;
+        float* corr = a.corr ? a.corr + (size_t)row * a.out_pitch : nullptr;
+        // nxcorr_dev for the lane's R pixels at once (same arithmetic), so each of the two
+        // passes is one round of loads in flight instead of R
+        const size_t pp = a.plane_pitch;
+        const int n = a.n;
+        const TIn* p0[R];
+        const TIn* p1[R];
+        bool live[R];
+        int first[R];
+        uint32_t sl[R], sr[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int c0 = col0_base + r * 64;
+            first[r] = (int)(glo[r] & 0xFFFFu);
+            const bool dup = NODUPES && (int)(0xFFFFu - (ghi[r] & 0xFFFFu)) != first[r];
+            live[r] = c0 < cols && !dup;
+            p0[r] = s0 + (c0 < cols ? c0 : 0);
+            p1[r] = s1 + (live[r] ? first[r] : 0);
+            sl[r] = 0;
+            sr[r] = 0;
+        }
+        for (int t = 0; t < n; ++t)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                sl[r] += ld(p0[r] + t * pp);
+                sr[r] += ld(p1[r] + t * pp);
+            }
+        float m0[R], m1[R], cov[R], v0[R], v1[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            m0[r] = div_p((float)sl[r], (float)n);
+            m1[r] = div_p((float)sr[r], (float)n);
+            cov[r] = v0[r] = v1[r] = 0.f;
+        }
+        for (int t = 0; t < n; ++t)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const float x0 = (float)ld(p0[r] + t * pp) - m0[r];
+                const float x1 = (float)ld(p1[r] + t * pp) - m1[r];
+                cov[r] = fma_p(x0, x1, cov[r]);
+                v0[r] = fma_p(x0, x0, v0[r]);
+                v1[r] = fma_p(x1, x1, v1[r]);
+            }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int c0 = col0_base + r * 64;
+            if (c0 >= cols) continue;
+            float o = -32768.f;
+            float cr = __builtin_nanf("");
+            if (live[r]) {
+                if (a.has_minvar && (v0[r] < a.minvar || v1[r] < a.minvar))
+                    cr = -1.f;
+                else
+                    cr = div_p(cov[r], sqrt_p(v0[r] * v1[r]));
+                if (!(cr < a.threshold)) o = (float)(c0 - first[r]);  // NaN passes
+            }
+            outf[c0] = o;
+            if (corr) corr[c0] = cr;
+        }
+        return;
+    }
     int16_t* __restrict__ out = a.out + (size_t)row * a.out_pitch;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -1406,6 +1482,18 @@ hipError_t launch_search16_r(const SearchArgs& a, int waves, hipStream_t st) {
     const size_t merge = a.split > 1 ? (size_t)(waves / a.split) * 64 * (2 * RP) * 8 * (a.split - 1) : 0;
     const size_t lds = stage > merge ? stage : merge;
     const int nwg = a.rows * a.tiles_per_row;
+    if constexpr (NODUPES && STEP == 0) {
+        if (a.out_f32) {
+            if (a.depth == 1)
+                hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP, STEP, 1>), dim3(nwg),
+                                   dim3(64 * waves), lds, st, a);
+            else
+                hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP, STEP, 2>), dim3(nwg),
+                                   dim3(64 * waves), lds, st, a);
+            return hipGetLastError();
+        }
+    }
+    if (a.out_f32) return hipErrorInvalidValue;  // fused agree: NoDuplicates, variant 16 only
     hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP, STEP>), dim3(nwg), dim3(64 * waves), lds,
                        st, a);
     return hipGetLastError();
@@ -1562,6 +1650,8 @@ hipError_t launch_search(SearchArgs a, const SearchGeometry& g, int words, bool 
     a.tiles_per_row = g.tiles_per_row;
     a.split = g.split;
     if (g.waves % g.split) return hipErrorInvalidValue;
+    if (a.out_f32 && (g.variant != 16 || !nodupes || (a.depth != 1 && a.depth != 2)))
+        return hipErrorInvalidValue;  // the fused agree epilogue exists for these only
     switch (words) {
         case 1: return launch_search_w<1>(a, nodupes, g, st);
         case 2: return launch_search_w<2>(a, nodupes, g, st);

@@ -35,6 +35,18 @@ struct SearchArgs {
     // fused Consistency (launch_search_lr): per-tile column minima [rows][tiles][cols]
     uint32_t* rev_first = nullptr;
     uint32_t* rev_last = nullptr;  // NoDuplicates only
+    // fused NXC agree (launch_search with out_f32 set; NoDuplicates search, no subpixel,
+    // single precision): the epilogue correlates each pixel with its best match and
+    // writes the float disparity (-32768 invalid) and the corrmap instead of `out`
+    float* out_f32 = nullptr;
+    float* corr = nullptr;          // may be null
+    const void* stack0 = nullptr;
+    const void* stack1 = nullptr;
+    int n = 0, depth = 0;
+    size_t row_pitch = 0, plane_pitch = 0;
+    float threshold = 0.f;
+    int has_minvar = 0;
+    float minvar = 0.f;             // already scaled by n
 };
 
 struct SearchGeometry {

@@ -322,6 +322,30 @@ def test_fused_consistency_edges(gpu, oracle, n, H, W, maxval, no_dupes):
         same(d, rd)
 
 
+# The NXC agree fused into the search epilogue (what match runs without Consistency /
+# subpixel / DOUBLE) == the search followed by the separate agree kernel, byte for byte.
+@pytest.mark.parametrize("n,H,W,dt,minvar", [(8, 5, 700, np.uint8, None), (17, 4, 1300, np.uint16, 1.5),
+                                             (33, 6, 2048, np.uint8, 2.0), (40, 3, 900, np.uint8, None)])
+def test_fused_search_agree_equals_separate(gpu, n, H, W, dt, minvar):
+    from libbicos_amd.device import descriptor_words
+    L, R = stereo_stack(n, H, W, dt, dmin=3, drange=30, seed=n + W)
+    L[:, 1, 100:140] = 7  # flat patch: variance 0 -> NaN correlation / min-variance reject
+    s0, s1 = dev(L), dev(R)
+    words = descriptor_words(n, 0)
+    d0, d1 = gpu.transform(s0, 0, words), gpu.transform(s1, 0, words)
+    mv = None if minvar is None else float(np.float32(minvar) * np.float32(n))
+    for tune in [(0, 0, 0, 0), (16, 4, 8, 0), (16, 2, 8, 4)]:
+        gpu.tune(*tune)
+        try:
+            fo, fc = gpu.search_agree(d0, d1, s0, s1, words, 0.8, minvar_scaled=mv)
+            raw = gpu.search(d0, d1, W, words, 1)
+            so, sc = gpu.agree(raw, s0, s1, 0.8, mv)
+        finally:
+            gpu.tune(0, 0, 0, 0)
+        same(host(fo), host(so))
+        same(host(fc), host(sc))
+
+
 def test_errors(gpu):
     import torch
     from libbicos_amd import BicosError

@@ -21,6 +21,8 @@ for step in "$@"; do
         pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
         pytestk) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
         bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
+        benchnf) BICOS_FUSE_AGREE=0 run benchnf 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-path ;;
+        benchf) run benchf 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-path ;;
         bench3) run bench3 600 python bench.py --config cfg3 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
         ab1|ab3|ab2|ab4)  # A/B on one box: current lib vs build/alt.so (same bench, interleaved twice)
             c=cfg${step#ab}
