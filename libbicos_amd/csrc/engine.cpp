@@ -102,6 +102,28 @@ bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, in
                                       e->tune_waves, e->tune_split, e->cus);
 }
 
+// Search implementation: the matrix-core search (search_mx.hip) unless the engine is tuned
+// to a VALU variant (bicos_engine_tune variant 16/17/18/32) or BICOS_SEARCH=valu;
+// BICOS_SEARCH=mx forces it. Results are identical either way.
+bool use_mx(const bicos_engine* e) {
+    static const int env = [] {
+        const char* v = std::getenv("BICOS_SEARCH");
+        if (!v) return 0;
+        if (!std::strcmp(v, "valu")) return 1;
+        if (!std::strcmp(v, "mx")) return 2;
+        return 0;
+    }();
+    if (e && e->tune_variant == 64) return true;
+    if (e && e->tune_variant != 0) return false;
+    return env != 1;
+}
+
+bicos_hip::MxGeometry mx_geometry(const bicos_engine* e, int rows, int cols, int words) {
+    const bool tuned = e && e->tune_variant == 64;
+    return bicos_hip::search_mx_geometry(rows, cols, words, 64 * 1024, tuned ? e->tune_R : 0,
+                                         tuned ? e->tune_waves : 0, e ? e->cus : 256);
+}
+
 bool fused_consistency() {
     // one fused forward+reverse search (search_lr_kernel) unless BICOS_CONSISTENCY=twopass
     // asks for a forward and a full reverse search (A/B; identical results)
@@ -189,7 +211,8 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     const bool nodupes = consistency ? cfg.no_dupes != 0 : true;
     const bool dbl = cfg.precision != 0;
 
-    const bool fused = consistency && fused_consistency();
+    const bool mx = use_mx(e);
+    const bool fused = consistency && !mx && fused_consistency();
     const bicos_hip::SearchGeometry glr =
         fused ? geometry_lr(e, rows, cols, words, nodupes) : bicos_hip::SearchGeometry{};
 
@@ -236,8 +259,8 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
         return !(v && !std::strcmp(v, "0"));
     }();
     const bool has_step_ = has_nxcorr && cfg.subpixel_step >= 0;
-    const bool fuse_agree = fuse_env && !consistency && has_nxcorr && !has_step_ && !dbl &&
-                            g.variant == 16;
+    const bool fuse_agree = fuse_env && !mx && !consistency && has_nxcorr && !has_step_ &&
+                            !dbl && g.variant == 16;
     if (fuse_agree) {
         bicos_hip::SearchArgs sa{d0, d1, nullptr, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
         sa.out_f32 = (float*)disp;
@@ -254,7 +277,27 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
         return check_hip(bicos_hip::launch_search(sa, g, words, true, st),
                          "search + agree launch");
     }
-    if (!consistency) {
+    if (mx) {
+        const bicos_hip::MxGeometry gm = mx_geometry(e, rows, cols, words);
+        if (!consistency) {
+            bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
+            rc = check_hip(bicos_hip::launch_search_mx(sa, gm, words, true, st), "search launch");
+            if (rc) return rc;
+        } else {
+            // forward and full reverse search (reverse = the same search with the stacks
+            // swapped, bicos.hpp:96), then the left-right check
+            bicos_hip::SearchArgs fa{d0, d1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
+            rc = check_hip(bicos_hip::launch_search_mx(fa, gm, words, nodupes, st), "search launch");
+            if (rc) return rc;
+            bicos_hip::SearchArgs ra{d1, d0, rev, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
+            rc = check_hip(bicos_hip::launch_search_mx(ra, gm, words, nodupes, st),
+                           "reverse search launch");
+            if (rc) return rc;
+            bicos_hip::ConsistencyArgs ca{fwd, rev, raw, rows, cols, (size_t)cols, cfg.max_lr_diff};
+            rc = check_hip(bicos_hip::launch_consistency(ca, st), "consistency launch");
+            if (rc) return rc;
+        }
+    } else if (!consistency) {
         bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
         rc = check_hip(bicos_hip::launch_search(sa, g, words, true, st), "search launch");
         if (rc) return rc;
@@ -618,8 +661,18 @@ void bicos_engine_destroy(bicos_engine* e) {
 
 int bicos_engine_tune(bicos_engine* e, int variant, int col0_per_lane, int waves, int split) {
     if (!e) return fail(BICOS_E_ARG, "null engine");
+    if (variant == 64) {  // matrix-core search: col0_per_lane = 32-column tiles per wave
+        if (col0_per_lane != 0 && col0_per_lane != 2 && col0_per_lane != 4 && col0_per_lane != 8)
+            return fail(BICOS_E_ARG, "variant 64: tiles per wave 2|4|8");
+        if (waves < 0 || waves > 8) return fail(BICOS_E_ARG, "waves 1..8");
+        e->tune_variant = 64;
+        e->tune_R = col0_per_lane;
+        e->tune_waves = waves;
+        e->tune_split = 0;
+        return BICOS_OK;
+    }
     if (variant != 0 && variant != 16 && variant != 17 && variant != 18 && variant != 32)
-        return fail(BICOS_E_ARG, "variant 0|16|17|18|32");
+        return fail(BICOS_E_ARG, "variant 0|16|17|18|32|64");
     const int v = (variant == 17 || variant == 18) ? 16 : (variant ? variant : 16);
     if (col0_per_lane != 0 && !(v == 16 ? (col0_per_lane == 2 || col0_per_lane == 4)
                                         : (col0_per_lane == 1 || col0_per_lane == 2 ||
@@ -724,13 +777,18 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     const size_t dpitch = bicos_desc_pitch(cols, words);
     const bool nodupes = (flags & 1) != 0;
     const bicos_hip::SearchGeometry g = geometry(e, rows, cols, words);
+    const bool mx = use_mx(e);
     if (!(flags & 2)) {
         bicos_hip::SearchArgs sa{desc0, desc1, out, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
+        if (mx)
+            return check_hip(bicos_hip::launch_search_mx(sa, mx_geometry(e, rows, cols, words),
+                                                         words, nodupes, st),
+                             "search launch");
         return check_hip(bicos_hip::launch_search(sa, g, words, nodupes, st), "search launch");
     }
     if (!e) return fail(BICOS_E_ARG, "consistency search needs an engine workspace");
     const size_t map16 = align_up((size_t)rows * cols * 2);
-    if (fused_consistency()) {
+    if (!mx && fused_consistency()) {
         const bicos_hip::SearchGeometry glr = geometry_lr(e, rows, cols, words, nodupes);
         const size_t keys = align_up((size_t)rows * glr.tiles_per_row * cols * 4);
         int rc = reserve(e->ws, e->ws_bytes, map16 + keys * (nodupes ? 2 : 1), e->device);
@@ -757,13 +815,28 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     }
     int rc = reserve(e->ws, e->ws_bytes, 2 * map16, e->device);
     if (rc) return rc;
+    rc = check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent");
+    if (rc) return rc;
+    struct MarkUse {
+        hipEvent_t ev;
+        hipStream_t st;
+        ~MarkUse() { (void)hipEventRecord(ev, st); }
+    } mark{e->ws_ready, st};
     int16_t* fwd = (int16_t*)e->ws;
     int16_t* rev = (int16_t*)((char*)e->ws + map16);
     bicos_hip::SearchArgs fa{desc0, desc1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
-    rc = check_hip(bicos_hip::launch_search(fa, g, words, nodupes, st), "search launch");
-    if (rc) return rc;
     bicos_hip::SearchArgs ra{desc1, desc0, rev, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
-    rc = check_hip(bicos_hip::launch_search(ra, g, words, nodupes, st), "reverse search launch");
+    if (mx) {
+        const bicos_hip::MxGeometry gm = mx_geometry(e, rows, cols, words);
+        rc = check_hip(bicos_hip::launch_search_mx(fa, gm, words, nodupes, st), "search launch");
+        if (rc) return rc;
+        rc = check_hip(bicos_hip::launch_search_mx(ra, gm, words, nodupes, st),
+                       "reverse search launch");
+    } else {
+        rc = check_hip(bicos_hip::launch_search(fa, g, words, nodupes, st), "search launch");
+        if (rc) return rc;
+        rc = check_hip(bicos_hip::launch_search(ra, g, words, nodupes, st), "reverse search launch");
+    }
     if (rc) return rc;
     bicos_hip::ConsistencyArgs ca{fwd, rev, out, rows, cols, (size_t)cols, max_lr_diff};
     return check_hip(bicos_hip::launch_consistency(ca, st), "consistency launch");
@@ -855,8 +928,9 @@ int bicos_subpixel_device(const int16_t* raw, const void* stack0, const void* st
 }
 
 const char* bicos_build_info(void) {
-    return "libbicos_amd: gfx950 HIP kernels (transform, LDS-broadcast popcount/argmin search, "
-           "NXC agree/subpixel), -O3 -ffp-contract=off";
+    return "libbicos_amd: gfx950 HIP kernels (transform, mx search: FP4 MFMA Hamming products "
+           "with argmin keys in the accumulator [default], LDS-broadcast popcount/argmin VALU "
+           "search, NXC agree/subpixel), -O3 -ffp-contract=off";
 }
 
 }  // extern "C"

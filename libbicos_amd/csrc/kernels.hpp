@@ -102,6 +102,19 @@ hipError_t launch_consistency(const ConsistencyArgs& a, hipStream_t st);
 hipError_t launch_search_lr(SearchArgs a, const SearchGeometry& g, int words, bool nodupes,
                             hipStream_t st);
 hipError_t launch_consistency_keys(const ConsistencyArgs& a, hipStream_t st);
+
+// Matrix-core search (search_mx.hip): FP4 MFMA Hamming products, argmin keys in the
+// accumulator. Same outputs as launch_search (a.out, a.out_mode); no fused agree.
+struct MxGeometry {
+    int chunk;              // col1 per LDS fill (multiple of 32)
+    int waves;              // waves per workgroup
+    int T;                  // 32-col0 tiles per wave (2, 4, 8)
+    int tiles_per_row;      // workgroups per row
+};
+MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int T = 0,
+                              int waves = 0, int cus = 256);
+hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool nodupes,
+                            hipStream_t st);
 hipError_t launch_agree(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
 hipError_t launch_subpixel(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
 

@@ -425,7 +425,8 @@ def test_search_tuning_settings_are_exact(gpu, oracle, words):
         b[..., 7] &= 0x7FFFFFFF
     lo = _low_entropy_desc(H, W, words, 3)
     settings = [(32, 1, 4, 0), (32, 2, 8, 0), (32, 4, 2, 0), (16, 2, 8, 1), (16, 2, 8, 2),
-                (16, 2, 8, 4), (16, 4, 4, 2), (16, 4, 8, 4), (16, 2, 1, 1), (16, 2, 2, 2)]
+                (16, 2, 8, 4), (16, 4, 4, 2), (16, 4, 8, 4), (16, 2, 1, 1), (16, 2, 2, 2),
+                (64, 2, 8, 0), (64, 4, 8, 0), (64, 8, 8, 0), (64, 2, 1, 0), (64, 8, 4, 0)]
     try:
         for flags, lr in ((1, -1), (3, 1), (2, 2)):
             for (x, y) in ((a, b), (lo, lo[:, ::-1].copy())):
@@ -436,3 +437,37 @@ def test_search_tuning_settings_are_exact(gpu, oracle, words):
                     same(out, ref)
     finally:
         gpu.tune(0, 0, 0, 0)
+
+
+# Matrix-core search (search_mx.hip): extreme Hamming keys (x = +-255: all-zero left vs
+# all-one right descriptors), rows that are not a multiple of the 32-column block, rows
+# wider than one LDS chunk, every tile count -- against the oracle and the VALU search.
+@pytest.mark.parametrize("words", [1, 2, 4, 8])
+@pytest.mark.parametrize("W", [1, 31, 33, 95, 2049, 4111])
+def test_mx_search_edges(gpu, oracle, words, W):
+    H = 3
+    rng = np.random.default_rng(W * 10 + words)
+    a = rng.integers(0, 2 ** 32, size=(H, W, words), dtype=np.uint64).astype(np.uint32)
+    b = a[:, np.roll(np.arange(W), 5)] ^ (rng.random((H, W, words)) < 0.05).astype(np.uint32)
+    full = np.uint32(0xFFFFFFFF)
+    a[0, : W // 2] = 0          # left all zero, right all one: the extreme keys
+    b[0, W // 3:] = full
+    b[1] = full                 # every col1 ties: the minimum is duplicated everywhere
+    if words == 8:
+        a[..., 7] &= 0x7FFFFFFF
+        b[..., 7] &= 0x7FFFFFFF
+    try:
+        for flags, lr in ((1, -1), (0, -1), (3, 1), (2, 0)):
+            ref = oracle.search(a, b, flags, lr)
+            for s in [(64, 2, 8, 0), (64, 8, 8, 0), (64, 4, 2, 0), (16, 0, 0, 0)]:
+                gpu.tune(*s)
+                out = host(gpu.search(dev(_pack(a)), dev(_pack(b)), W, words, flags, lr))
+                same(out, ref)
+    finally:
+        gpu.tune(0, 0, 0, 0)
+
+
+def test_mx_is_the_default_search(gpu):
+    """The engine runs the matrix-core search unless tuned to a VALU variant."""
+    from libbicos_amd import _lib
+    assert "mx" in _lib.lib().bicos_build_info().decode()

@@ -18,7 +18,7 @@ for step in "$@"; do
         valu) run valu 120 ./build/valu_peak ;;
         dep) run dep 200 ./build/dep_bench ;;
         smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
-        pytest) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+        pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
         pytestk) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
         bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
         benchnf) BICOS_FUSE_AGREE=0 run benchnf 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-path ;;
