@@ -97,7 +97,8 @@ bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, in
             max_lds = std::min(max_lds, chunk * words * 4);
         }
     }
-    if (!e) return bicos_hip::search_geometry(rows, cols, words, max_lds);
+    // (an engine tuned for the matrix-core search runs VALU kernels untuned)
+    if (!e || e->tune_variant >= 64) return bicos_hip::search_geometry(rows, cols, words, max_lds);
     return bicos_hip::search_geometry(rows, cols, words, max_lds, e->tune_variant, e->tune_R,
                                       e->tune_waves, e->tune_split, e->cus);
 }
@@ -113,15 +114,18 @@ bool use_mx(const bicos_engine* e) {
         if (!std::strcmp(v, "mx")) return 2;
         return 0;
     }();
-    if (e && e->tune_variant == 64) return true;
+    if (e && e->tune_variant >= 64) return true;
     if (e && e->tune_variant != 0) return false;
     return env != 1;
 }
 
 bicos_hip::MxGeometry mx_geometry(const bicos_engine* e, int rows, int cols, int words) {
-    const bool tuned = e && e->tune_variant == 64;
-    return bicos_hip::search_mx_geometry(rows, cols, words, 64 * 1024, tuned ? e->tune_R : 0,
-                                         tuned ? e->tune_waves : 0, e ? e->cus : 256);
+    const bool tuned = e && e->tune_variant >= 64;
+    // tuned: split = LDS stage KiB (0 = 64)
+    const int lds = tuned && e->tune_split > 0 ? e->tune_split * 1024 : 64 * 1024;
+    return bicos_hip::search_mx_geometry(rows, cols, words, lds, tuned ? e->tune_R : 0,
+                                         tuned ? e->tune_waves : 0, e ? e->cus : 256,
+                                         tuned ? e->tune_variant - 64 : 0);
 }
 
 bool fused_consistency() {
@@ -141,7 +145,8 @@ bicos_hip::SearchGeometry geometry_lr(const bicos_engine* e, int rows, int cols,
     const int limit = e ? e->lds_limit : 64 * 1024;
     const int budget = limit < 80 * 1024 ? limit : 80 * 1024;
     const int extra = 4 * (nodupes ? 2 : 1);
-    if (!e) return bicos_hip::search_geometry(rows, cols, words, budget, 16, 4, 0, 0, 256, extra);
+    if (!e || e->tune_variant >= 64)
+        return bicos_hip::search_geometry(rows, cols, words, budget, 16, 4, 0, 0, 256, extra);
     // 4 col0 per lane by default: the per-col1 wave reduction amortises over more pairs
     const int R = (e->tune_R == 2 || e->tune_R == 4) ? e->tune_R : 4;
     return bicos_hip::search_geometry(rows, cols, words, budget, 16, R, e->tune_waves,
@@ -251,7 +256,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     if (rc) return rc;
 
     // 2. bicos search (cpu.cpp:68-75)
-    const bicos_hip::SearchGeometry g = geometry(e, rows, cols, words);
+    const bicos_hip::SearchGeometry g = mx ? bicos_hip::SearchGeometry{} : geometry(e, rows, cols, words);
     // NXC agree fused into the search epilogue (no Consistency, no subpixel, single
     // precision, default search variant) unless BICOS_FUSE_AGREE=0
     static const bool fuse_env = [] {
@@ -661,18 +666,22 @@ void bicos_engine_destroy(bicos_engine* e) {
 
 int bicos_engine_tune(bicos_engine* e, int variant, int col0_per_lane, int waves, int split) {
     if (!e) return fail(BICOS_E_ARG, "null engine");
-    if (variant == 64) {  // matrix-core search: col0_per_lane = 32-column tiles per wave
+    if (variant >= 64 && variant <= 70 && variant != 67) {
+        // matrix-core search (64 auto keys, 65 one product + xor keys, 66 two products;
+        // +4: software-pipelined block loop);
+        // col0_per_lane = 32-column tiles per wave
         if (col0_per_lane != 0 && col0_per_lane != 2 && col0_per_lane != 4 && col0_per_lane != 8)
-            return fail(BICOS_E_ARG, "variant 64: tiles per wave 2|4|8");
+            return fail(BICOS_E_ARG, "variant 64-70: tiles per wave 2|4|8");
         if (waves < 0 || waves > 8) return fail(BICOS_E_ARG, "waves 1..8");
-        e->tune_variant = 64;
+        if (split < 0 || split > 160) return fail(BICOS_E_ARG, "variant 64-70: split = LDS KiB 0..160");
+        e->tune_variant = variant;
         e->tune_R = col0_per_lane;
         e->tune_waves = waves;
-        e->tune_split = 0;
+        e->tune_split = split;
         return BICOS_OK;
     }
     if (variant != 0 && variant != 16 && variant != 17 && variant != 18 && variant != 32)
-        return fail(BICOS_E_ARG, "variant 0|16|17|18|32|64");
+        return fail(BICOS_E_ARG, "variant 0|16|17|18|32|64..70");
     const int v = (variant == 17 || variant == 18) ? 16 : (variant ? variant : 16);
     if (col0_per_lane != 0 && !(v == 16 ? (col0_per_lane == 2 || col0_per_lane == 4)
                                         : (col0_per_lane == 1 || col0_per_lane == 2 ||
@@ -776,8 +785,8 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     hipStream_t st = (hipStream_t)stream;
     const size_t dpitch = bicos_desc_pitch(cols, words);
     const bool nodupes = (flags & 1) != 0;
-    const bicos_hip::SearchGeometry g = geometry(e, rows, cols, words);
     const bool mx = use_mx(e);
+    const bicos_hip::SearchGeometry g = mx ? bicos_hip::SearchGeometry{} : geometry(e, rows, cols, words);
     if (!(flags & 2)) {
         bicos_hip::SearchArgs sa{desc0, desc1, out, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
         if (mx)

@@ -48,6 +48,15 @@ constexpr float KEY_BIAS = 256.f;
 constexpr float KEY_EPS = 1.f / 32768.f;  // col1 * 2^-15
 constexpr float KEY_PAD = 1.0e30f;        // C of columns beyond the image (A = 0 there)
 
+// One-product keys (XK): C = 768 + col1 * 2^-14 keeps every D1 = 768 + x + col1 * 2^-14 in
+// the binade [512, 1024) (|x| <= 255), where the ulp is 2^-14: the low 14 mantissa bits of
+// D1 ARE col1 and the bits above are x + 256. So bits(D1) ^ 0x3FFF orders by x, then by
+// DEScending col1, and its minimum is the last minimum: NoDuplicates costs one v_xor per
+// pair instead of a second (negated) product. Needs cols <= 16384.
+constexpr float XK_BIAS = 768.f;
+constexpr float XK_EPS = 1.f / 16384.f;
+constexpr uint32_t XK_COL = 0x3FFFu;
+
 // nibble p of the result = bit p of `b` (b < 256): 1 -> 0x1
 __device__ __forceinline__ uint32_t spread8(uint32_t b) {
     uint32_t t = (b | (b << 12)) & 0x000F000Fu;
@@ -72,6 +81,26 @@ __device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) {
     return max(max(a, b), c);
 }
 
+__device__ __forceinline__ uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
+__device__ __forceinline__ float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
+
+// min over the 16 keys of a D tile (bits ^ flip) and m; depth-3 tree of v_min3_u32
+__device__ __forceinline__ uint32_t min16(const v16f& d, uint32_t m, uint32_t flip) {
+    // (element copied first: __builtin_bit_cast of a vector-element lvalue reads element 0)
+    auto k = [&](int r) { return fbits(d[r]) ^ flip; };
+    const uint32_t a0 = umin3(k(0), k(1), k(2)), a1 = umin3(k(3), k(4), k(5));
+    const uint32_t a2 = umin3(k(6), k(7), k(8)), a3 = umin3(k(9), k(10), k(11));
+    const uint32_t a4 = umin3(k(12), k(13), k(14));
+    return umin3(m, umin3(a0, a1, a2), umin3(a3, a4, k(15)));
+}
+__device__ __forceinline__ uint32_t max16(const v16f& d, uint32_t m) {
+    auto k = [&](int r) { return fbits(d[r]); };
+    const uint32_t a0 = umax3(k(0), k(1), k(2)), a1 = umax3(k(3), k(4), k(5));
+    const uint32_t a2 = umax3(k(6), k(7), k(8)), a3 = umax3(k(9), k(10), k(11));
+    const uint32_t a4 = umax3(k(12), k(13), k(14));
+    return umax3(m, umax3(a0, a1, a2), umax3(a3, a4, k(15)));
+}
+
 __device__ __forceinline__ v16f mfma_fp4(v4i a, v4i b, v16f c) {
     const v8i a8 = {a[0], a[1], a[2], a[3], 0, 0, 0, 0};
     const v8i b8 = {b[0], b[1], b[2], b[3], 0, 0, 0, 0};
@@ -79,8 +108,6 @@ __device__ __forceinline__ v16f mfma_fp4(v4i a, v4i b, v16f c) {
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 0, 0, 0);
 }
 
-__device__ __forceinline__ uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
-__device__ __forceinline__ float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
 
 // col1 encoded in a key (D1 or D2 bits): key - 256 = +-x + col1 * 2^-15, x integer
 __device__ __forceinline__ int key_col(uint32_t key) {
@@ -88,8 +115,13 @@ __device__ __forceinline__ int key_col(uint32_t key) {
     return (int)((v - floorf(v)) * 32768.f);
 }
 
-template <int WORDS, bool NODUPES, int T>
-__global__ __launch_bounds__(512) void search_mx_kernel(SearchArgs a) {
+// waves per SIMD the register allocation must allow: 4 (two 8-wave workgroups per CU)
+// without the pipeline, 2 with it
+template <int WORDS, bool NODUPES, int T, bool XK, bool PIPE>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(PIPE ? 2 : 4)))
+void search_mx_kernel(SearchArgs a) {
+    constexpr float BIAS = XK ? XK_BIAS : KEY_BIAS;
+    constexpr float EPS = XK ? XK_EPS : KEY_EPS;
     constexpr int KS = WORDS >= 2 ? WORDS / 2 : 1;  // 64-bit K-steps
     constexpr int WL = 2 * KS;                      // LDS word slots per col1 (W=1: 1 pad)
     extern __shared__ __attribute__((aligned(16))) v4i lds_mx[];  // [WL][chunk]
@@ -136,40 +168,31 @@ __global__ __launch_bounds__(512) void search_mx_kernel(SearchArgs a) {
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         m1[t] = 0xFFFFFFFFu;
-        m2[t] = 0u;
+        m2[t] = XK ? 0xFFFFFFFFu : 0u;
     }
 
     // row offset of accumulator register r in this lane half
     auto rrow = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; };
 
-    // one 32-col1 block against the wave's T tiles
-    auto block = [&](const v4i* af, const v16f& c1, const v16f& c2) {
-        v4i an[KS];
-        if constexpr (NODUPES) {
+    // PIPE: software pipeline over 32-col1 blocks -- the products of block b+1 for tile t are
+    // issued right after tile t's block-b keys are reduced, so a wave's MFMAs run under its
+    // own reductions (one live D tile per tile). Without PIPE each product is reduced right
+    // away: fewer registers, more resident waves hide the latency instead.
+    v16f d[T], e[T];
+    auto products = [&](int t, const v4i* af, const v4i* an, const v16f& c1, const v16f& c2) {
+        d[t] = mfma_fp4(af[0], bf[t][0], c1);
 #pragma unroll
-            for (int s = 0; s < KS; ++s)
+        for (int s = 1; s < KS; ++s) d[t] = mfma_fp4(af[s], bf[t][s], d[t]);
+        if constexpr (NODUPES && !XK) {
+            e[t] = mfma_fp4(an[0], bf[t][0], c2);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) an[s][q] = af[s][q] | (af[s][q] << 2);  // 1.0 -> -1.0
+            for (int s = 1; s < KS; ++s) e[t] = mfma_fp4(an[s], bf[t][s], e[t]);
         }
-#pragma unroll
-        for (int t = 0; t < T; ++t) {
-            v16f d = mfma_fp4(af[0], bf[t][0], c1);
-#pragma unroll
-            for (int s = 1; s < KS; ++s) d = mfma_fp4(af[s], bf[t][s], d);
-            uint32_t m = m1[t];
-#pragma unroll
-            for (int r = 0; r < 16; r += 2) m = umin3(m, fbits(d[r]), fbits(d[r + 1]));
-            m1[t] = m;
-            if constexpr (NODUPES) {
-                v16f e = mfma_fp4(an[0], bf[t][0], c2);
-#pragma unroll
-                for (int s = 1; s < KS; ++s) e = mfma_fp4(an[s], bf[t][s], e);
-                uint32_t M = m2[t];
-#pragma unroll
-                for (int r = 0; r < 16; r += 2) M = umax3(M, fbits(e[r]), fbits(e[r + 1]));
-                m2[t] = M;
-            }
-        }
+    };
+    auto reduce = [&](int t) {
+        m1[t] = min16(d[t], m1[t], 0u);
+        if constexpr (NODUPES && XK) m2[t] = min16(d[t], m2[t], XK_COL);
+        else if constexpr (NODUPES) m2[t] = max16(e[t], m2[t]);
     };
 
     const bool idle = c0_wave >= cols;  // wave-uniform; still joins the barriers
@@ -194,32 +217,68 @@ __global__ __launch_bounds__(512) void search_mx_kernel(SearchArgs a) {
         __syncthreads();
         if (idle) continue;
 
-        v16f cc;
+        const int nfull = ncols / 32;
+        const bool partial = (ncols & 31) != 0;
+        v16f cc;  // C of the current block: BIAS + col1 * EPS
 #pragma unroll
-        for (int r = 0; r < 16; ++r) cc[r] = KEY_BIAS + (float)(base + rrow(r)) * KEY_EPS;
-        const int full = ncols / 32;
-        for (int b = 0; b < full; ++b) {
-            v4i af[KS];
-#pragma unroll
-            for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + 32 * b + j];
-            block(af, cc, cc);
-#pragma unroll
-            for (int r = 0; r < 16; ++r) cc[r] += 32.f * KEY_EPS;  // exact (< 512)
-        }
-        if (ncols % 32) {
-            // columns beyond the image: A = 0 there, so D1 = KEY_PAD, D2 = 0 never win
-            const int b = full;
-            v4i af[KS];
+        for (int r = 0; r < 16; ++r) cc[r] = BIAS + (float)(base + rrow(r)) * EPS;
+        auto fragments = [&](int b, v4i* af, v4i* an) {
 #pragma unroll
             for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + 32 * b + j];
-            v16f c1, c2;
+            if constexpr (NODUPES && !XK) {
+#pragma unroll
+                for (int s = 0; s < KS; ++s)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) an[s][q] = af[s][q] | (af[s][q] << 2);  // 1.0 -> -1.0
+            }
+        };
+        // C of a block reaching past the image: A = 0 there, so D1 = KEY_PAD, D2 = 0 never win
+        auto masked = [&](int b, v16f& c1, v16f& c2) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
                 const bool in = 32 * b + rrow(r) < ncols;
                 c1[r] = in ? cc[r] : KEY_PAD;
                 c2[r] = in ? cc[r] : 0.f;
             }
-            block(af, c1, c2);
+        };
+        // one block: PIPE reduces tile t's previous block and issues its next products;
+        // otherwise products then keys, tile by tile (fewer live registers, more waves)
+        auto blockop = [&](int b, const v16f& c1, const v16f& c2, bool first) {
+            v4i af[KS], an[KS];
+            fragments(b, af, an);
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                if constexpr (PIPE) {
+                    if (!first) reduce(t);
+                    products(t, af, an, c1, c2);
+                } else {
+                    products(t, af, an, c1, c2);
+                    reduce(t);
+                }
+            }
+        };
+        if (nfull == 0) {
+            v16f c1, c2;
+            masked(0, c1, c2);
+            blockop(0, c1, c2, true);
+        } else {
+            blockop(0, cc, cc, true);
+        }
+        for (int b = 1; b < nfull; ++b) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cc[r] += 32.f * EPS;  // exact (same binade)
+            blockop(b, cc, cc, false);
+        }
+        if (partial && nfull > 0) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cc[r] += 32.f * EPS;
+            v16f c1, c2;
+            masked(nfull, c1, c2);
+            blockop(nfull, c1, c2, false);
+        }
+        if constexpr (PIPE) {
+#pragma unroll
+            for (int t = 0; t < T; ++t) reduce(t);
         }
     }
     if (idle) return;
@@ -228,7 +287,8 @@ __global__ __launch_bounds__(512) void search_mx_kernel(SearchArgs a) {
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         m1[t] = min(m1[t], (uint32_t)__shfl_xor((int)m1[t], 32));
-        if constexpr (NODUPES) m2[t] = max(m2[t], (uint32_t)__shfl_xor((int)m2[t], 32));
+        if constexpr (NODUPES && XK) m2[t] = min(m2[t], (uint32_t)__shfl_xor((int)m2[t], 32));
+        else if constexpr (NODUPES) m2[t] = max(m2[t], (uint32_t)__shfl_xor((int)m2[t], 32));
     }
     int16_t* out = a.out + (size_t)row * a.out_pitch;
 #pragma unroll
@@ -236,9 +296,10 @@ __global__ __launch_bounds__(512) void search_mx_kernel(SearchArgs a) {
         if ((t & 1) != h) continue;  // half 0 writes even tiles, half 1 odd tiles
         const int c0 = c0_wave + 32 * t + j;
         if (c0 >= cols) continue;
-        const int best = key_col(m1[t]);
+        const int best = XK ? (int)(m1[t] & XK_COL) : key_col(m1[t]);
         bool ok = true;
-        if constexpr (NODUPES) ok = key_col(m2[t]) == best;
+        if constexpr (NODUPES && XK) ok = (int)((m2[t] & XK_COL) ^ XK_COL) == best;
+        else if constexpr (NODUPES) ok = key_col(m2[t]) == best;
         int16_t v;
         if (a.out_mode == 0)
             v = ok ? (int16_t)(c0 - best) : INVALID_I16;
@@ -248,11 +309,11 @@ __global__ __launch_bounds__(512) void search_mx_kernel(SearchArgs a) {
     }
 }
 
-template <int WORDS, bool NODUPES, int T>
+template <int WORDS, bool NODUPES, int T, bool XK, bool PIPE>
 hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     constexpr int WL = WORDS >= 2 ? WORDS : 2;
     const size_t lds = (size_t)WL * a.chunk * 16;
-    const auto kern = search_mx_kernel<WORDS, NODUPES, T>;
+    const auto kern = search_mx_kernel<WORDS, NODUPES, T, XK, PIPE>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -262,14 +323,44 @@ hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int WORDS, bool NODUPES>
-hipError_t launch_mx_t(const SearchArgs& a, const MxGeometry& g, hipStream_t st) {
+// Tile counts whose registers fit without scratch (checked with
+// -Rpass-analysis=kernel-resource-usage): 8 tiles only for 32/64-bit descriptors with one
+// key product (the pipeline keeps a 16-register D tile per tile live).
+constexpr bool mx_tiles_fit(int words, bool nodupes, bool xk, int t) {
+    return t <= 4 || (words == 1 && (xk || !nodupes)) || (words == 2 && !nodupes);
+}
+
+template <int WORDS, bool NODUPES, bool XK, bool PIPE>
+hipError_t launch_mx_p(const SearchArgs& a, const MxGeometry& g, hipStream_t st) {
+    if (g.T == 8) {
+        if constexpr (mx_tiles_fit(WORDS, NODUPES, XK, 8) && !PIPE) {
+            return launch_mx<WORDS, NODUPES, 8, XK, PIPE>(a, g.waves, st);
+        } else {  // does not fit: 4 tiles per wave, twice the workgroups per row
+            SearchArgs b = a;
+            const long per_wg = 32L * g.waves * 4;
+            b.tiles_per_row = (int)((a.cols + per_wg - 1) / per_wg);
+            return launch_mx<WORDS, NODUPES, 4, XK, PIPE>(b, g.waves, st);
+        }
+    }
     switch (g.T) {
-        case 2: return launch_mx<WORDS, NODUPES, 2>(a, g.waves, st);
-        case 4: return launch_mx<WORDS, NODUPES, 4>(a, g.waves, st);
-        case 8: return launch_mx<WORDS, NODUPES, 8>(a, g.waves, st);
+        case 2: return launch_mx<WORDS, NODUPES, 2, XK, PIPE>(a, g.waves, st);
+        case 4: return launch_mx<WORDS, NODUPES, 4, XK, PIPE>(a, g.waves, st);
     }
     return hipErrorInvalidValue;
+}
+
+template <int WORDS, bool NODUPES, bool XK>
+hipError_t launch_mx_k(const SearchArgs& a, const MxGeometry& g, hipStream_t st) {
+    return g.pipe ? launch_mx_p<WORDS, NODUPES, XK, true>(a, g, st)
+                  : launch_mx_p<WORDS, NODUPES, XK, false>(a, g, st);
+}
+
+template <int WORDS, bool NODUPES>
+hipError_t launch_mx_t(const SearchArgs& a, const MxGeometry& g, hipStream_t st) {
+    // without NoDuplicates both key forms are one product; the XK form also needs no
+    // float decode. The two-product form covers rows wider than 16384.
+    if (g.keys == 1 && a.cols <= 16384) return launch_mx_k<WORDS, NODUPES, true>(a, g, st);
+    return launch_mx_k<WORDS, NODUPES, false>(a, g, st);
 }
 
 template <int WORDS>
@@ -280,8 +371,10 @@ hipError_t launch_mx_w(const SearchArgs& a, const MxGeometry& g, bool nodupes, h
 }  // namespace
 
 MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int T, int waves,
-                              int cus) {
+                              int cus, int keys) {
     MxGeometry g;
+    g.keys = (keys & 3) == 2 ? 2 : 1;
+    g.pipe = (keys & 4) != 0;
     const int wl = words >= 2 ? words : 2;
     // LDS chunk of expanded right descriptors (16 B per word per col1), multiple of 32
     int chunk = lds_bytes / (wl * 16);
@@ -293,10 +386,10 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     if (T) {
         g.T = T;
     } else {
-        // the largest T (fewest right-row expansions per row) that still gives every CU
-        // about two workgroups
+        // 4 tiles per wave (8 spill for most widths), 2 when the grid would not give every
+        // CU about two workgroups (narrow row bands)
         g.T = 2;
-        for (int t = 8; t >= 2; t /= 2) {
+        for (int t = 4; t >= 2; t /= 2) {
             const long per_wg = 32L * g.waves * t;
             const long nwg = (long)rows * ((cols + per_wg - 1) / per_wg);
             if (nwg >= 2L * (cus > 0 ? cus : 256)) {

@@ -426,7 +426,8 @@ def test_search_tuning_settings_are_exact(gpu, oracle, words):
     lo = _low_entropy_desc(H, W, words, 3)
     settings = [(32, 1, 4, 0), (32, 2, 8, 0), (32, 4, 2, 0), (16, 2, 8, 1), (16, 2, 8, 2),
                 (16, 2, 8, 4), (16, 4, 4, 2), (16, 4, 8, 4), (16, 2, 1, 1), (16, 2, 2, 2),
-                (64, 2, 8, 0), (64, 4, 8, 0), (64, 8, 8, 0), (64, 2, 1, 0), (64, 8, 4, 0)]
+                (64, 2, 8, 0), (64, 4, 8, 0), (64, 8, 8, 0), (64, 2, 1, 0), (64, 8, 4, 0),
+                (65, 8, 8, 0), (65, 2, 4, 0), (66, 8, 8, 0), (66, 4, 2, 0)]
     try:
         for flags, lr in ((1, -1), (3, 1), (2, 2)):
             for (x, y) in ((a, b), (lo, lo[:, ::-1].copy())):
@@ -443,7 +444,7 @@ def test_search_tuning_settings_are_exact(gpu, oracle, words):
 # all-one right descriptors), rows that are not a multiple of the 32-column block, rows
 # wider than one LDS chunk, every tile count -- against the oracle and the VALU search.
 @pytest.mark.parametrize("words", [1, 2, 4, 8])
-@pytest.mark.parametrize("W", [1, 31, 33, 95, 2049, 4111])
+@pytest.mark.parametrize("W", [1, 31, 33, 95, 2049, 4111, 16385])
 def test_mx_search_edges(gpu, oracle, words, W):
     H = 3
     rng = np.random.default_rng(W * 10 + words)
@@ -459,7 +460,7 @@ def test_mx_search_edges(gpu, oracle, words, W):
     try:
         for flags, lr in ((1, -1), (0, -1), (3, 1), (2, 0)):
             ref = oracle.search(a, b, flags, lr)
-            for s in [(64, 2, 8, 0), (64, 8, 8, 0), (64, 4, 2, 0), (16, 0, 0, 0)]:
+            for s in [(64, 2, 8, 0), (65, 8, 8, 0), (66, 8, 8, 0), (66, 4, 2, 0), (16, 0, 0, 0)]:
                 gpu.tune(*s)
                 out = host(gpu.search(dev(_pack(a)), dev(_pack(b)), W, words, flags, lr))
                 same(out, ref)
