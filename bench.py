@@ -13,10 +13,13 @@ completed before the closing barrier.
 
 Extra keys on the JSON line:
   roofline      the dominant kernel (the Hamming search), timed live with HIP
-                events on the stream it runs on; algorithmic INT32 lane-ops per
-                launch / average launch time vs the VALU peak (the search is
-                VALU-bound, not HBM- or MFMA-bound: DESIGN.md s5). `hbm` holds the
-                HBM-bound stages (transform, agree) against the 8 TB/s peak.
+                events on the stream it runs on. Default (matrix-core search,
+                search_mx.hip): algorithmic FP4 MFMA FLOPs per launch (2 x descriptor
+                bits per Hamming pair) / average launch time vs the dense FP4 MFMA
+                peak; `valu_view` holds the key-reduction issue bound that actually
+                binds it. BICOS_SEARCH=valu: pairs/s vs the VALU
+                issue bound of the popcount search. `hbm` holds the HBM-bound stages
+                (transform, agree) against the 8 TB/s peak.
   cpu_baseline  the C oracle (oracle/bicos_oracle.c, -march=x86-64-v3) on this
                 host's cores, rank 0 at N=1 only, over a bounded row sample.
 """
@@ -40,6 +43,9 @@ HBM_PEAK_GBS = 8000.0
 VALU_FULL_TOPS = 72.0
 VALU_HALF_TOPS = 38.5
 VALU_NOMINAL_TOPS = 256 * 128 * 2.4e9 / 1e12   # 78.6: every op at full rate, 2.4 GHz
+# Dense FP4 MFMA peak (MI355X_MICROARCH.md "Peak FP6/FP4 MFMA": ~10 PF dense, the 20 PF
+# figure is 2:1 sparsity): v_mfma_scale_f32_32x32x64_f8f6f4 on FP4 operands.
+MFMA_FP4_DENSE_TFLOPS = 10000.0
 
 CONFIGS = {
     # BASELINE.json configs; "cfg2" is the one the headline metric is quoted on
@@ -94,6 +100,32 @@ def search_ops(rows: int, W: int, words: int, cfg: dict) -> float:
     xor + `words` bcnt + key pack + min (+ med3 with NoDuplicates) = 2w+3 (2w+2 without)."""
     dupes = cfg.get("variant", 0) == 0 or cfg.get("no_dupes", False)
     return search_pairs(rows, W, cfg) * (2 * words + (3 if dupes else 2))
+
+
+def mx_search() -> bool:
+    """The pipeline's search runs on the matrix cores unless BICOS_SEARCH=valu
+    (engine.cpp use_mx)."""
+    return os.environ.get("BICOS_SEARCH", "") != "valu"
+
+
+def mx_flops(rows: int, W: int, words: int, cfg: dict):
+    """(algorithmic, executed) FLOPs of the matrix-core search per launch. Each Hamming
+    pair is a K-long dot product, K = descriptor bits (2K FLOPs); the MFMA executes K
+    padded to its 64-bit steps. Consistency runs the forward and the reverse search."""
+    passes = 2 if cfg.get("variant", 0) == 1 else 1
+    pairs = search_pairs(rows, W, cfg) * passes
+    return pairs * 2 * 32 * words, pairs * 2 * 64 * max(1, words // 2)
+
+
+def mx_key_pair_peak(words: int, cfg: dict) -> float:
+    """Issue bound in pairs/s of the matrix-core search's VALU key reduction at the
+    measured rates: per pair 1/2 v_min3 (half rate) for the first minimum and, with
+    NoDuplicates, one v_xor (full) + 1/2 v_min3 for the last minimum; per 32-pair tile
+    column 1-2 integer adds (full; negligible)."""
+    dupes = cfg.get("variant", 0) == 0 or cfg.get("no_dupes", False)
+    full = 1.0 if dupes else 0.0
+    half = 1.0 if dupes else 0.5
+    return 1.0 / (full / (VALU_FULL_TOPS * 1e12) + half / (VALU_HALF_TOPS * 1e12))
 
 
 def load_traffic(kernel_prefix: str, rows: int, W: int):
@@ -267,9 +299,12 @@ def main():
     # the pipeline fuses the NXC agree into the search epilogue when there is no
     # Consistency / subpixel / DOUBLE (engine.cpp match_device): time that launch then
     mc = C["cfg"]
+    # (engine.cpp match_device: with the VALU search unless BICOS_FUSE_AGREE=0; with the
+    # matrix-core search only when BICOS_FUSE_AGREE=1)
+    fuse_env = os.environ.get("BICOS_FUSE_AGREE", "")
     fused_agree = (mcfg.variant == 0 and mcfg.nxcorr_threshold is not None and
                    not mc.get("subpixel_step") and not mcfg.precision and
-                   os.environ.get("BICOS_FUSE_AGREE", "1") != "0")
+                   (fuse_env == "1" if mx_search() else fuse_env != "0"))
     mv = mc.get("min_variance")
     mv = None if mv is None or mv < 0 else mv * n
 
@@ -313,31 +348,68 @@ def main():
     ag_bytes = rows * W * (2 + 8) + rows * W * valid * 2 * n
     # algorithmic bytes of one search launch: both descriptor bands + the int16 output
     search_bytes = rows * W * (2 * 4 * words + 2)
-    traffic = load_traffic("search16_kernel", rows, W) if args.config == "cfg2" and rows == H else None
-
-    roof = {
-        "kernel": ("search_lr_kernel<%d words> (fused forward + reverse Hamming argmin)" % words
-                   if C["cfg"].get("variant", 0) == 1 else
-                   "search16_kernel<%d words> (Hamming argmin, packed 16-bit keys)%s" %
-                   (words, " + fused NXC agree epilogue" if fused_agree else "")),
-        "bound": "valu",
-        "achieved": round(achieved, 1),
-        "peak": round(peak, 1),
-        "unit": "Gpairs/s",
-        "frac": round(achieved / peak, 4),
-        "traffic": None if traffic is None else traffic["bytes"],
-        "traffic_source": None if traffic is None else traffic["source"],
-        "algorithmic_bytes": search_bytes,
-        "pairs_per_launch": pairs,
-        "ms_per_launch": round(t_search * 1e3, 4),
-        "peak_model": "issue bound of the per-pair VALU mix at measured rates "
-                      "(full %.1f / half %.1f T lane-op/s); see DESIGN.md s5" %
-                      (VALU_FULL_TOPS, VALU_HALF_TOPS),
-        "lane_ops_view": {
-            "achieved_Tops": round(search_ops(rows, W, words, C["cfg"]) / t_search / 1e12, 2),
-            "nominal_peak_Tops": round(VALU_NOMINAL_TOPS, 1),
-            "ops_model": "one pass over the cost matrix, 32-bit keys: 2w+3 (2w+2) lane-ops per pair",
-        },
+    mx = mx_search()
+    cons = C["cfg"].get("variant", 0) == 1
+    kname = "search_mx_kernel" if mx else ("search_lr_kernel" if cons else "search16_kernel")
+    traffic = load_traffic(kname, rows, W) if args.config == "cfg2" and rows == H else None
+    if mx:
+        alg_flops, exe_flops = mx_flops(rows, W, words, C["cfg"])
+        achieved_tf = alg_flops / t_search / 1e12
+        kpeak = mx_key_pair_peak(words, C["cfg"]) / 1e9
+        evaluated = pairs * (2 if cons else 1)
+        roof = {
+            "kernel": ("search_mx_kernel<%d words> x2 (forward + reverse FP4 MFMA Hamming argmin) "
+                       "+ consistency_kernel" % words if cons else
+                       "search_mx_kernel<%d words> (FP4 MFMA Hamming products, argmin keys in the "
+                       "accumulator)%s" % (words, " + fused NXC agree epilogue" if fused_agree else "")),
+            "bound": "mfma",
+            "achieved": round(achieved_tf, 1),
+            "peak": MFMA_FP4_DENSE_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved_tf / MFMA_FP4_DENSE_TFLOPS, 4),
+            "traffic": None if traffic is None else traffic["bytes"],
+            "traffic_source": None if traffic is None else traffic["source"],
+            "algorithmic_bytes": search_bytes,
+            "algorithmic_flops": alg_flops,
+            "executed_flops": exe_flops,
+            "pairs_per_launch": evaluated,
+            "ms_per_launch": round(t_search * 1e3, 4),
+            "peak_model": "dense FP4 MFMA peak (MI355X_MICROARCH.md); algorithmic FLOPs = "
+                          "2 x descriptor bits per Hamming pair",
+            "valu_view": {
+                "what": "the VALU key reduction (v_min3 + v_xor per pair) that bounds the "
+                        "kernel; issue bound at the measured rates, see DESIGN.md s5",
+                "achieved_Gpairs": round(evaluated / t_search / 1e9, 1),
+                "peak_Gpairs": round(kpeak, 1),
+                "frac": round(evaluated / t_search / 1e9 / kpeak, 4),
+            },
+        }
+    else:
+        roof = {
+            "kernel": ("search_lr_kernel<%d words> (fused forward + reverse Hamming argmin)" % words
+                       if cons else
+                       "search16_kernel<%d words> (Hamming argmin, packed 16-bit keys)%s" %
+                       (words, " + fused NXC agree epilogue" if fused_agree else "")),
+            "bound": "valu",
+            "achieved": round(achieved, 1),
+            "peak": round(peak, 1),
+            "unit": "Gpairs/s",
+            "frac": round(achieved / peak, 4),
+            "traffic": None if traffic is None else traffic["bytes"],
+            "traffic_source": None if traffic is None else traffic["source"],
+            "algorithmic_bytes": search_bytes,
+            "pairs_per_launch": pairs,
+            "ms_per_launch": round(t_search * 1e3, 4),
+            "peak_model": "issue bound of the per-pair VALU mix at measured rates "
+                          "(full %.1f / half %.1f T lane-op/s); see DESIGN.md s5" %
+                          (VALU_FULL_TOPS, VALU_HALF_TOPS),
+            "lane_ops_view": {
+                "achieved_Tops": round(search_ops(rows, W, words, C["cfg"]) / t_search / 1e12, 2),
+                "nominal_peak_Tops": round(VALU_NOMINAL_TOPS, 1),
+                "ops_model": "one pass over the cost matrix, 32-bit keys: 2w+3 (2w+2) lane-ops per pair",
+            },
+        }
+    roof.update({
         "hbm": {
             "transform_GBps": round(tf_bytes / t_tf / 1e9, 1),
             "transform_frac": round(tf_bytes / t_tf / 1e9 / HBM_PEAK_GBS, 4),
@@ -349,7 +421,7 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
         },
-    }
+    })
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -128,6 +128,23 @@ bicos_hip::MxGeometry mx_geometry(const bicos_engine* e, int rows, int cols, int
                                          tuned ? e->tune_variant - 64 : 0);
 }
 
+// The NoDuplicates search with the NXC agree fused into its epilogue (sa.out_f32 set): the
+// matrix-core kernel unless BICOS_SEARCH=valu / a VALU tuning; a software-pipelined
+// matrix-core tuning runs unpipelined here, a non-default VALU variant runs variant 16.
+int launch_search_agree(const bicos_engine* e, const bicos_hip::SearchArgs& sa, int words,
+                        hipStream_t st) {
+    if (use_mx(e)) {
+        bicos_hip::MxGeometry gm = mx_geometry(e, sa.rows, sa.cols, words);
+        gm.pipe = false;
+        return check_hip(bicos_hip::launch_search_mx(sa, gm, words, true, st),
+                         "search + agree launch");
+    }
+    bicos_hip::SearchGeometry g = geometry(e, sa.rows, sa.cols, words);
+    if (g.variant != 16)
+        g = bicos_hip::search_geometry(sa.rows, sa.cols, words, e ? e->max_lds : 64 * 1024);
+    return check_hip(bicos_hip::launch_search(sa, g, words, true, st), "search + agree launch");
+}
+
 bool fused_consistency() {
     // one fused forward+reverse search (search_lr_kernel) unless BICOS_CONSISTENCY=twopass
     // asks for a forward and a full reverse search (A/B; identical results)
@@ -258,14 +275,18 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     // 2. bicos search (cpu.cpp:68-75)
     const bicos_hip::SearchGeometry g = mx ? bicos_hip::SearchGeometry{} : geometry(e, rows, cols, words);
     // NXC agree fused into the search epilogue (no Consistency, no subpixel, single
-    // precision, default search variant) unless BICOS_FUSE_AGREE=0
-    static const bool fuse_env = [] {
+    // precision): BICOS_FUSE_AGREE unset = with the VALU search (variant 16) only -- the
+    // matrix-core search runs faster with the separate agree kernel (measured: cfg2 fused
+    // 0.580 ms vs 0.437 + 0.061 separate); 1 = with either search; 0 = never
+    static const int fuse_env = [] {
         const char* v = std::getenv("BICOS_FUSE_AGREE");
-        return !(v && !std::strcmp(v, "0"));
+        if (v && !std::strcmp(v, "0")) return 0;
+        if (v && !std::strcmp(v, "1")) return 2;
+        return 1;
     }();
     const bool has_step_ = has_nxcorr && cfg.subpixel_step >= 0;
-    const bool fuse_agree = fuse_env && !mx && !consistency && has_nxcorr && !has_step_ &&
-                            !dbl && g.variant == 16;
+    const bool fuse_agree = fuse_env && !consistency && has_nxcorr && !has_step_ && !dbl &&
+                            (mx ? fuse_env == 2 : g.variant == 16);
     if (fuse_agree) {
         bicos_hip::SearchArgs sa{d0, d1, nullptr, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
         sa.out_f32 = (float*)disp;
@@ -279,8 +300,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
         sa.threshold = threshold;
         sa.has_minvar = cfg.min_variance >= 0;
         sa.minvar = sa.has_minvar ? cfg.min_variance * (float)n : 0.f;  // cpu.cpp:127
-        return check_hip(bicos_hip::launch_search(sa, g, words, true, st),
-                         "search + agree launch");
+        return launch_search_agree(e, sa, words, st);
     }
     if (mx) {
         const bicos_hip::MxGeometry gm = mx_geometry(e, rows, cols, words);
@@ -865,8 +885,6 @@ int bicos_search_agree_device(bicos_engine* e, const uint32_t* desc0, const uint
     if (!desc0 || !desc1 || !stack0 || !stack1 || !out) return fail(BICOS_E_ARG, "null buffer");
     if (row_pitch < (size_t)cols || plane_pitch < (size_t)rows * row_pitch)
         return fail(BICOS_E_ARG, "row/plane pitch smaller than the image");
-    bicos_hip::SearchGeometry g = geometry(e, rows, cols, words);
-    if (g.variant != 16) g = bicos_hip::search_geometry(rows, cols, words, e ? e->max_lds : 64 * 1024);
     bicos_hip::SearchArgs sa{desc0, desc1, nullptr, rows, cols, bicos_desc_pitch(cols, words),
                              (size_t)cols, 0, 0, 0};
     sa.out_f32 = out;
@@ -880,8 +898,7 @@ int bicos_search_agree_device(bicos_engine* e, const uint32_t* desc0, const uint
     sa.threshold = threshold;
     sa.has_minvar = has_minvar;
     sa.minvar = minvar_scaled;
-    return check_hip(bicos_hip::launch_search(sa, g, words, true, (hipStream_t)stream),
-                     "search + agree launch");
+    return launch_search_agree(e, sa, words, (hipStream_t)stream);
 }
 
 static int agree_common(bool sub, const int16_t* raw, const void* stack0, const void* stack1,

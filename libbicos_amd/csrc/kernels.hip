@@ -16,6 +16,7 @@
 // performs is an explicit IEEE round-to-nearest op (no contraction, correctly rounded
 // division and sqrt), fmaf exactly where the reference calls std::fmaf.
 #include "kernels.hpp"
+#include "nxc.hpp"
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -44,10 +45,10 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
     return max(min(a, b), min(max(a, b), c));
 }
 
-template <typename T>
-__device__ __forceinline__ uint32_t ld(const T* p) {
-    return (uint32_t)__builtin_nontemporal_load(p);
-}
+using nxc::ld;
+using nxc::fma_p;
+using nxc::div_p;
+using nxc::sqrt_p;
 
 // Raw buffer loads of an image stack: 128-bit resource built from uniform values, uniform
 // (SGPR) byte offset of the plane/row, 32-bit per-lane byte offset -- no VALU address math
@@ -638,10 +639,6 @@ __device__ __forceinline__ void search16_step(const uint32_t* s, uint32_t seed,
     }
 }
 
-__device__ __forceinline__ float fma_p(float a, float b, float c);
-__device__ __forceinline__ float div_p(float a, float b);
-__device__ __forceinline__ float sqrt_p(float x);
-
 // FUSE: 0 = plain search (int16 `out`), 1 / 2 = fused NXC agree epilogue on u8 / u16
 // stacks (agree.hpp:53-93 for the pixels this workgroup owns; see SearchArgs)
 template <int WORDS, bool NODUPES, int RP, int STEP, int FUSE = 0>
@@ -774,64 +771,18 @@ __global__ __launch_bounds__(512) void search16_kernel(SearchArgs a) {
         const TIn* s1 = (const TIn*)a.stack1 + (size_t)row * a.row_pitch;
         float* outf = a.out_f32 + (size_t)row * a.out_pitch;
         float* corr = a.corr ? a.corr + (size_t)row * a.out_pitch : nullptr;
-        // nxcorr_dev for the lane's R pixels at once (same arithmetic), so each of the two
-        // passes is one round of loads in flight instead of R
-        const size_t pp = a.plane_pitch;
-        const int n = a.n;
-        const TIn* p0[R];
-        const TIn* p1[R];
-        bool live[R];
-        int first[R];
-        uint32_t sl[R], sr[R];
+        int c0[R], best[R];
+        bool in[R], live[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int c0 = col0_base + r * 64;
-            first[r] = (int)(glo[r] & 0xFFFFu);
-            const bool dup = NODUPES && (int)(0xFFFFu - (ghi[r] & 0xFFFFu)) != first[r];
-            live[r] = c0 < cols && !dup;
-            p0[r] = s0 + (c0 < cols ? c0 : 0);
-            p1[r] = s1 + (live[r] ? first[r] : 0);
-            sl[r] = 0;
-            sr[r] = 0;
+            c0[r] = col0_base + r * 64;
+            best[r] = (int)(glo[r] & 0xFFFFu);
+            const bool dup = NODUPES && (int)(0xFFFFu - (ghi[r] & 0xFFFFu)) != best[r];
+            in[r] = c0[r] < cols;
+            live[r] = in[r] && !dup;
         }
-        for (int t = 0; t < n; ++t)
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                sl[r] += ld(p0[r] + t * pp);
-                sr[r] += ld(p1[r] + t * pp);
-            }
-        float m0[R], m1[R], cov[R], v0[R], v1[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            m0[r] = div_p((float)sl[r], (float)n);
-            m1[r] = div_p((float)sr[r], (float)n);
-            cov[r] = v0[r] = v1[r] = 0.f;
-        }
-        for (int t = 0; t < n; ++t)
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const float x0 = (float)ld(p0[r] + t * pp) - m0[r];
-                const float x1 = (float)ld(p1[r] + t * pp) - m1[r];
-                cov[r] = fma_p(x0, x1, cov[r]);
-                v0[r] = fma_p(x0, x0, v0[r]);
-                v1[r] = fma_p(x1, x1, v1[r]);
-            }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const int c0 = col0_base + r * 64;
-            if (c0 >= cols) continue;
-            float o = -32768.f;
-            float cr = __builtin_nanf("");
-            if (live[r]) {
-                if (a.has_minvar && (v0[r] < a.minvar || v1[r] < a.minvar))
-                    cr = -1.f;
-                else
-                    cr = div_p(cov[r], sqrt_p(v0[r] * v1[r]));
-                if (!(cr < a.threshold)) o = (float)(c0 - first[r]);  // NaN passes
-            }
-            outf[c0] = o;
-            if (corr) corr[c0] = cr;
-        }
+        nxc::agree_pixels<TIn, R>(s0, s1, a.plane_pitch, a.n, c0, best, in, live, a.threshold,
+                                  a.has_minvar, a.minvar, outf, corr);
         return;
     }
     int16_t* __restrict__ out = a.out + (size_t)row * a.out_pitch;
@@ -1093,30 +1044,7 @@ __global__ __launch_bounds__(256) void consistency_kernel(ConsistencyArgs a) {
 
 // ---------------------------------------------------------------------- agree
 
-__device__ __forceinline__ float fma_p(float a, float b, float c) { return __builtin_fmaf(a, b, c); }
-__device__ __forceinline__ double fma_p(double a, double b, double c) { return __builtin_fma(a, b, c); }
-__device__ __forceinline__ float div_p(float a, float b) { return __fdiv_rn(a, b); }
-__device__ __forceinline__ double div_p(double a, double b) { return __ddiv_rn(a, b); }
-// Correctly rounded sqrtf. hipcc lowers __fsqrt_rn / sqrtf to a bare v_sqrt_f32 (up to
-// 1 ulp off) here; the reference's std::sqrt is IEEE. Fix the estimate s with the residuals
-// of its two float neighbours (x - s_dn*s <= 0 -> s_dn; x - s_up*s > 0 -> s_up), after
-// scaling tiny inputs into the normal range.
-__device__ __forceinline__ float sqrt_p(float x) {
-    const bool tiny = x < 0x1.0p-96f;
-    const float xs = tiny ? x * 0x1.0p+32f : x;
-    float s = __builtin_amdgcn_sqrtf(xs);
-    const int si = __float_as_int(s);
-    const float s_dn = __int_as_float(si - 1);
-    const float s_up = __int_as_float(si + 1);
-    const float r_dn = __builtin_fmaf(-s_dn, s, xs);
-    const float r_up = __builtin_fmaf(-s_up, s, xs);
-    s = r_dn <= 0.f ? s_dn : s;
-    s = r_up > 0.f ? s_up : s;
-    s = tiny ? s * 0x1.0p-16f : s;
-    // zero, +inf and NaN (and negative) pass through the hardware result
-    return (xs == 0.f || xs == __builtin_inff() || !(xs > 0.f)) ? __builtin_amdgcn_sqrtf(x) : s;
-}
-__device__ __forceinline__ double sqrt_p(double a) { return __dsqrt_rn(a); }
+// fma_p / div_p / sqrt_p (IEEE, correctly rounded): nxc.hpp
 
 // nxcorr (agree.hpp:28-51): means from exact integer sums (< 2^24, identical to the
 // reference's sequential float sums); centred samples, three fma chains in t order,

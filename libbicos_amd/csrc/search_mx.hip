@@ -30,9 +30,12 @@
 // ds_read_b128 per lane. Accumulator map (32x32 shapes): lane l, register r holds row
 // (r & 3) + 8 (r >> 2) + 4 (l >> 5) (= col1 in the block) and column l & 31 (= col0).
 #include "kernels.hpp"
+#include "nxc.hpp"
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <type_traits>
 
 namespace bicos_hip {
 
@@ -56,6 +59,15 @@ constexpr float KEY_PAD = 1.0e30f;        // C of columns beyond the image (A = 
 constexpr float XK_BIAS = 768.f;
 constexpr float XK_EPS = 1.f / 16384.f;
 constexpr uint32_t XK_COL = 0x3FFFu;
+// XK keys are block-relative: C is the same for every block, C = 768 + (XK_K0 + col1 % 32)
+// * 2^-14, and the running minima are kept relative to the base col1 B of the block being
+// reduced -- their col1 field is col1 - B + XK_K0 (first minimum) and 31 - (col1 - B) (last
+// minimum, key ^ 0x3FFF), moved by -32 / +32 per block with ONE integer add each. Both
+// fields stay inside [0, 16383] for B <= 16352 (cols <= 16384). This replaces the 16 float
+// adds per block that advanced C (which the compiler packed into v_pk_add_f32, expensive
+// beside MFMAs) and keeps C in registers that never change.
+constexpr int XK_K0 = 16352;
+constexpr uint32_t XK_INF = 0x7F000000u;  // "no key yet"; stays huge under the shifts
 
 // nibble p of the result = bit p of `b` (b < 256): 1 -> 0x1
 __device__ __forceinline__ uint32_t spread8(uint32_t b) {
@@ -117,7 +129,9 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 
 // waves per SIMD the register allocation must allow: 4 (two 8-wave workgroups per CU)
 // without the pipeline, 2 with it
-template <int WORDS, bool NODUPES, int T, bool XK, bool PIPE>
+// FUSE: 0 = int16 `out`; 1 / 2 = NXC agree fused into the epilogue on u8 / u16 stacks
+// (agree.hpp:53-93 for the pixels the lane owns; float disparity + corrmap, see SearchArgs)
+template <int WORDS, bool NODUPES, int T, bool XK, bool PIPE, int FUSE = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(PIPE ? 2 : 4)))
 void search_mx_kernel(SearchArgs a) {
     constexpr float BIAS = XK ? XK_BIAS : KEY_BIAS;
@@ -167,8 +181,8 @@ void search_mx_kernel(SearchArgs a) {
     uint32_t m1[T], m2[T];
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-        m1[t] = 0xFFFFFFFFu;
-        m2[t] = XK ? 0xFFFFFFFFu : 0u;
+        m1[t] = XK ? XK_INF : 0xFFFFFFFFu;
+        m2[t] = XK ? XK_INF : 0u;
     }
 
     // row offset of accumulator register r in this lane half
@@ -189,11 +203,20 @@ void search_mx_kernel(SearchArgs a) {
             for (int s = 1; s < KS; ++s) e[t] = mfma_fp4(an[s], bf[t][s], e[t]);
         }
     };
+    // (XK: first move the running minima from the previous block's base to this one's)
     auto reduce = [&](int t) {
-        m1[t] = min16(d[t], m1[t], 0u);
-        if constexpr (NODUPES && XK) m2[t] = min16(d[t], m2[t], XK_COL);
-        else if constexpr (NODUPES) m2[t] = max16(e[t], m2[t]);
+        if constexpr (XK) {
+            m1[t] = min16(d[t], m1[t] - 32u, 0u);
+            if constexpr (NODUPES) m2[t] = min16(d[t], m2[t] + 32u, XK_COL);
+        } else {
+            m1[t] = min16(d[t], m1[t], 0u);
+            if constexpr (NODUPES) m2[t] = max16(e[t], m2[t]);
+        }
     };
+    // XK: the C of every block (col1 % 32 only)
+    v16f cx;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cx[r] = XK_BIAS + (float)(XK_K0 + rrow(r)) * XK_EPS;
 
     const bool idle = c0_wave >= cols;  // wave-uniform; still joins the barriers
     for (int base = 0; base < cols; base += chunk) {
@@ -219,9 +242,13 @@ void search_mx_kernel(SearchArgs a) {
 
         const int nfull = ncols / 32;
         const bool partial = (ncols & 31) != 0;
-        v16f cc;  // C of the current block: BIAS + col1 * EPS
+        v16f cc;  // C of the current block: BIAS + col1 * EPS (XK: cx, the same for all)
+        if constexpr (XK) {
+            cc = cx;
+        } else {
 #pragma unroll
-        for (int r = 0; r < 16; ++r) cc[r] = BIAS + (float)(base + rrow(r)) * EPS;
+            for (int r = 0; r < 16; ++r) cc[r] = BIAS + (float)(base + rrow(r)) * EPS;
+        }
         auto fragments = [&](int b, v4i* af, v4i* an) {
 #pragma unroll
             for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + 32 * b + j];
@@ -265,13 +292,17 @@ void search_mx_kernel(SearchArgs a) {
             blockop(0, cc, cc, true);
         }
         for (int b = 1; b < nfull; ++b) {
+            if constexpr (!XK) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) cc[r] += 32.f * EPS;  // exact (same binade)
+                for (int r = 0; r < 16; ++r) cc[r] += 32.f * EPS;  // exact (same binade)
+            }
             blockop(b, cc, cc, false);
         }
         if (partial && nfull > 0) {
+            if constexpr (!XK) {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) cc[r] += 32.f * EPS;
+                for (int r = 0; r < 16; ++r) cc[r] += 32.f * EPS;
+            }
             v16f c1, c2;
             masked(nfull, c1, c2);
             blockop(nfull, c1, c2, false);
@@ -290,16 +321,50 @@ void search_mx_kernel(SearchArgs a) {
         if constexpr (NODUPES && XK) m2[t] = min(m2[t], (uint32_t)__shfl_xor((int)m2[t], 32));
         else if constexpr (NODUPES) m2[t] = max(m2[t], (uint32_t)__shfl_xor((int)m2[t], 32));
     }
+    // best col1 of tile t, and whether it is the only column at the minimum cost
+    // XK: the minima are relative to the base of the last block
+    const int blast = ((cols + 31) & ~31) - 32;
+    auto best_of = [&](int t) {
+        return XK ? (int)(m1[t] & XK_COL) - XK_K0 + blast : key_col(m1[t]);
+    };
+    auto unique_of = [&](int t, int best) {
+        if constexpr (NODUPES && XK) return 31 - (int)(m2[t] & XK_COL) + blast == best;
+        else if constexpr (NODUPES) return key_col(m2[t]) == best;
+        return true;
+    };
+    if constexpr (FUSE != 0) {
+        // half 0 owns the even tiles, half 1 the odd ones: T/2 pixels per lane, correlated
+        // together with their best match straight from the stacks (no int16 map, no agree
+        // launch); col1 = best is always inside the row
+        using TIn = typename std::conditional<FUSE == 1, uint8_t, uint16_t>::type;
+        constexpr int TH = T / 2;
+        int c0[TH], best[TH];
+        bool in[TH], live[TH];
+#pragma unroll
+        for (int i = 0; i < TH; ++i) {
+            const int b0 = best_of(2 * i), b1 = best_of(2 * i + 1);
+            const bool u0 = unique_of(2 * i, b0), u1 = unique_of(2 * i + 1, b1);
+            c0[i] = c0_wave + 32 * (2 * i + h) + j;
+            best[i] = h ? b1 : b0;
+            in[i] = c0[i] < cols;
+            live[i] = in[i] && (h ? u1 : u0);
+        }
+        const TIn* s0 = (const TIn*)a.stack0 + (size_t)row * a.row_pitch;
+        const TIn* s1 = (const TIn*)a.stack1 + (size_t)row * a.row_pitch;
+        float* outf = a.out_f32 + (size_t)row * a.out_pitch;
+        float* corr = a.corr ? a.corr + (size_t)row * a.out_pitch : nullptr;
+        nxc::agree_pixels<TIn, TH>(s0, s1, a.plane_pitch, a.n, c0, best, in, live, a.threshold,
+                                   a.has_minvar, a.minvar, outf, corr);
+        return;
+    }
     int16_t* out = a.out + (size_t)row * a.out_pitch;
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         if ((t & 1) != h) continue;  // half 0 writes even tiles, half 1 odd tiles
         const int c0 = c0_wave + 32 * t + j;
         if (c0 >= cols) continue;
-        const int best = XK ? (int)(m1[t] & XK_COL) : key_col(m1[t]);
-        bool ok = true;
-        if constexpr (NODUPES && XK) ok = (int)((m2[t] & XK_COL) ^ XK_COL) == best;
-        else if constexpr (NODUPES) ok = key_col(m2[t]) == best;
+        const int best = best_of(t);
+        const bool ok = unique_of(t, best);
         int16_t v;
         if (a.out_mode == 0)
             v = ok ? (int16_t)(c0 - best) : INVALID_I16;
@@ -313,7 +378,17 @@ template <int WORDS, bool NODUPES, int T, bool XK, bool PIPE>
 hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     constexpr int WL = WORDS >= 2 ? WORDS : 2;
     const size_t lds = (size_t)WL * a.chunk * 16;
-    const auto kern = search_mx_kernel<WORDS, NODUPES, T, XK, PIPE>;
+    // fused agree only with the default NoDuplicates search (the pipeline's)
+    auto pick = [&]() {
+        if constexpr (NODUPES && !PIPE) {
+            if (a.out_f32) return a.depth == 2 ? search_mx_kernel<WORDS, NODUPES, T, XK, PIPE, 2>
+                                                : search_mx_kernel<WORDS, NODUPES, T, XK, PIPE, 1>;
+        }
+        return search_mx_kernel<WORDS, NODUPES, T, XK, PIPE, 0>;
+    };
+    if (a.out_f32 && (!NODUPES || PIPE || (a.depth != 1 && a.depth != 2)))
+        return hipErrorInvalidValue;
+    const auto kern = pick();
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -323,7 +323,8 @@ def test_fused_consistency_edges(gpu, oracle, n, H, W, maxval, no_dupes):
 
 
 # The NXC agree fused into the search epilogue (what match runs without Consistency /
-# subpixel / DOUBLE) == the search followed by the separate agree kernel, byte for byte.
+# subpixel / DOUBLE; search16_kernel or search_mx_kernel) == the search followed by the
+# separate agree kernel, byte for byte.
 @pytest.mark.parametrize("n,H,W,dt,minvar", [(8, 5, 700, np.uint8, None), (17, 4, 1300, np.uint16, 1.5),
                                              (33, 6, 2048, np.uint8, 2.0), (40, 3, 900, np.uint8, None)])
 def test_fused_search_agree_equals_separate(gpu, n, H, W, dt, minvar):
@@ -334,7 +335,9 @@ def test_fused_search_agree_equals_separate(gpu, n, H, W, dt, minvar):
     words = descriptor_words(n, 0)
     d0, d1 = gpu.transform(s0, 0, words), gpu.transform(s1, 0, words)
     mv = None if minvar is None else float(np.float32(minvar) * np.float32(n))
-    for tune in [(0, 0, 0, 0), (16, 4, 8, 0), (16, 2, 8, 4)]:
+    # default (matrix cores), VALU variants, matrix-core key forms / tile counts / pipeline
+    for tune in [(0, 0, 0, 0), (16, 4, 8, 0), (16, 2, 8, 4), (65, 2, 8, 0), (65, 8, 4, 0),
+                 (66, 4, 8, 0), (69, 4, 8, 0)]:
         gpu.tune(*tune)
         try:
             fo, fc = gpu.search_agree(d0, d1, s0, s1, words, 0.8, minvar_scaled=mv)
