@@ -129,13 +129,12 @@ bicos_hip::MxGeometry mx_geometry(const bicos_engine* e, int rows, int cols, int
 }
 
 // The NoDuplicates search with the NXC agree fused into its epilogue (sa.out_f32 set): the
-// matrix-core kernel unless BICOS_SEARCH=valu / a VALU tuning; a software-pipelined
-// matrix-core tuning runs unpipelined here, a non-default VALU variant runs variant 16.
+// matrix-core kernel unless BICOS_SEARCH=valu / a VALU tuning; a non-default VALU variant
+// runs variant 16.
 int launch_search_agree(const bicos_engine* e, const bicos_hip::SearchArgs& sa, int words,
                         hipStream_t st) {
     if (use_mx(e)) {
-        bicos_hip::MxGeometry gm = mx_geometry(e, sa.rows, sa.cols, words);
-        gm.pipe = false;
+        const bicos_hip::MxGeometry gm = mx_geometry(e, sa.rows, sa.cols, words);
         return check_hip(bicos_hip::launch_search_mx(sa, gm, words, true, st),
                          "search + agree launch");
     }
@@ -686,14 +685,13 @@ void bicos_engine_destroy(bicos_engine* e) {
 
 int bicos_engine_tune(bicos_engine* e, int variant, int col0_per_lane, int waves, int split) {
     if (!e) return fail(BICOS_E_ARG, "null engine");
-    if (variant >= 64 && variant <= 70 && variant != 67) {
-        // matrix-core search (64 auto keys, 65 one product + xor keys, 66 two products;
-        // +4: software-pipelined block loop);
+    if (variant >= 64 && variant <= 66) {
+        // matrix-core search (64 auto keys, 65 one product + xor keys, 66 two products);
         // col0_per_lane = 32-column tiles per wave
         if (col0_per_lane != 0 && col0_per_lane != 2 && col0_per_lane != 4 && col0_per_lane != 8)
-            return fail(BICOS_E_ARG, "variant 64-70: tiles per wave 2|4|8");
+            return fail(BICOS_E_ARG, "variant 64-66: tiles per wave 2|4|8");
         if (waves < 0 || waves > 8) return fail(BICOS_E_ARG, "waves 1..8");
-        if (split < 0 || split > 160) return fail(BICOS_E_ARG, "variant 64-70: split = LDS KiB 0..160");
+        if (split < 0 || split > 160) return fail(BICOS_E_ARG, "variant 64-66: split = LDS KiB 0..160");
         e->tune_variant = variant;
         e->tune_R = col0_per_lane;
         e->tune_waves = waves;
@@ -701,7 +699,7 @@ int bicos_engine_tune(bicos_engine* e, int variant, int col0_per_lane, int waves
         return BICOS_OK;
     }
     if (variant != 0 && variant != 16 && variant != 17 && variant != 18 && variant != 32)
-        return fail(BICOS_E_ARG, "variant 0|16|17|18|32|64..70");
+        return fail(BICOS_E_ARG, "variant 0|16|17|18|32|64|65|66");
     const int v = (variant == 17 || variant == 18) ? 16 : (variant ? variant : 16);
     if (col0_per_lane != 0 && !(v == 16 ? (col0_per_lane == 2 || col0_per_lane == 4)
                                         : (col0_per_lane == 1 || col0_per_lane == 2 ||

@@ -35,6 +35,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace bicos_hip {
@@ -68,6 +70,11 @@ constexpr uint32_t XK_COL = 0x3FFFu;
 // beside MFMAs) and keeps C in registers that never change.
 constexpr int XK_K0 = 16352;
 constexpr uint32_t XK_INF = 0x7F000000u;  // "no key yet"; stays huge under the shifts
+// KEYS 2 (any block order): the relative col1 fields span +-cols, so C carries a
+// mid-range offset instead -- first-minimum field col1 - B + 8160, last-minimum field
+// 8223 - (col1 - B) -- which keeps both in [0, 16383] for cols <= 8160.
+constexpr int XKF_K0 = 8160;
+constexpr int XKF_MAX_COLS = 8160;
 
 // nibble p of the result = bit p of `b` (b < 256): 1 -> 0x1
 __device__ __forceinline__ uint32_t spread8(uint32_t b) {
@@ -127,15 +134,32 @@ __device__ __forceinline__ int key_col(uint32_t key) {
     return (int)((v - floorf(v)) * 32768.f);
 }
 
-// waves per SIMD the register allocation must allow: 4 (two 8-wave workgroups per CU)
-// without the pipeline, 2 with it
+// KEYS: 0 = float keys (col1 * 2^-15 in C per block; NoDuplicates by a second, negated
+//           product), any width;
+//       1 = XK keys, blocks in ascending col1 order (cols <= 16384);
+//       2 = XK keys in any block order with the last-minimum work skipped where it cannot
+//           matter (NoDuplicates, cols <= 8160; see below).
 // FUSE: 0 = int16 `out`; 1 / 2 = NXC agree fused into the epilogue on u8 / u16 stacks
-// (agree.hpp:53-93 for the pixels the lane owns; float disparity + corrmap, see SearchArgs)
-template <int WORDS, bool NODUPES, int T, bool XK, bool PIPE, int FUSE = 0>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(PIPE ? 2 : 4)))
+// (agree.hpp:53-93 for the pixels the lane owns; float disparity + corrmap, see SearchArgs).
+//
+// KEYS 2. NoDuplicates needs the LAST column at the minimum cost only to compare it with
+// the first; a block none of whose keys reaches the running minimum cost cannot hold it. So
+// the running first minimum is shared by the two lane halves every block (v_permlane32_swap
+// + one v_min3), each half tests its own block minimum against it (<= in cost), and the
+// xor + min tree of the last minimum runs only when some lane of the wave passes. Blocks
+// are visited from the wave's own col0 downwards (chunks from the workgroup's, wrapping):
+// a stereo match lies at col1 <= col0 within a few blocks, the running minimum reaches it
+// early, and the rest of the row skips that half of the VALU work (cfg2 synthetic: ~6 % of
+// blocks still do it). The result is exact whatever the data: the order only changes speed.
+// Keys stay relative to the base B of the block being reduced (shifts by the signed
+// B - B_prev); C = 768 + (8160 + col1 % 32) * 2^-14 keeps both fields in [0, 16383].
+template <int WORDS, bool NODUPES, int T, int KEYS, int FUSE = 0>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void search_mx_kernel(SearchArgs a) {
-    constexpr float BIAS = XK ? XK_BIAS : KEY_BIAS;
-    constexpr float EPS = XK ? XK_EPS : KEY_EPS;
+    constexpr bool XK = KEYS != 0;
+    constexpr bool FREE = KEYS == 2;
+    static_assert(!FREE || NODUPES, "KEYS 2 is the NoDuplicates search");
+    constexpr int K0 = FREE ? XKF_K0 : XK_K0;
     constexpr int KS = WORDS >= 2 ? WORDS / 2 : 1;  // 64-bit K-steps
     constexpr int WL = 2 * KS;                      // LDS word slots per col1 (W=1: 1 pad)
     extern __shared__ __attribute__((aligned(16))) v4i lds_mx[];  // [WL][chunk]
@@ -179,19 +203,17 @@ void search_mx_kernel(SearchArgs a) {
     }
 
     uint32_t m1[T], m2[T];
+    int b2[T];  // KEYS 2: the base m2[t] is relative to (wave-uniform)
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         m1[t] = XK ? XK_INF : 0xFFFFFFFFu;
         m2[t] = XK ? XK_INF : 0u;
+        b2[t] = 0;
     }
 
     // row offset of accumulator register r in this lane half
     auto rrow = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; };
 
-    // PIPE: software pipeline over 32-col1 blocks -- the products of block b+1 for tile t are
-    // issued right after tile t's block-b keys are reduced, so a wave's MFMAs run under its
-    // own reductions (one live D tile per tile). Without PIPE each product is reduced right
-    // away: fewer registers, more resident waves hide the latency instead.
     v16f d[T], e[T];
     auto products = [&](int t, const v4i* af, const v4i* an, const v16f& c1, const v16f& c2) {
         d[t] = mfma_fp4(af[0], bf[t][0], c1);
@@ -203,9 +225,20 @@ void search_mx_kernel(SearchArgs a) {
             for (int s = 1; s < KS; ++s) e[t] = mfma_fp4(an[s], bf[t][s], e[t]);
         }
     };
-    // (XK: first move the running minima from the previous block's base to this one's)
-    auto reduce = [&](int t) {
-        if constexpr (XK) {
+    // block at base B, the previous one at base bp (XK: the running minima move from bp's
+    // frame to B's first)
+    auto reduce = [&](int t, int B, int bp) {
+        if constexpr (FREE) {
+            const uint32_t m1s = m1[t] - (uint32_t)(B - bp);
+            const uint32_t bm = min16(d[t], 0xFFFFFFFFu, 0u);   // this half's block minimum
+            const bool reach = bm <= (m1s | XK_COL);           // cost <= running minimum cost
+            const auto sw = __builtin_amdgcn_permlane32_swap(bm, bm, false, false);
+            m1[t] = umin3(m1s, sw[0], sw[1]);                  // both halves' minimum
+            if (__builtin_amdgcn_ballot_w64(reach)) {
+                m2[t] = min16(d[t], m2[t] + (uint32_t)(B - b2[t]), XK_COL);
+                b2[t] = B;
+            }
+        } else if constexpr (XK) {
             m1[t] = min16(d[t], m1[t] - 32u, 0u);
             if constexpr (NODUPES) m2[t] = min16(d[t], m2[t] + 32u, XK_COL);
         } else {
@@ -216,12 +249,20 @@ void search_mx_kernel(SearchArgs a) {
     // XK: the C of every block (col1 % 32 only)
     v16f cx;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) cx[r] = XK_BIAS + (float)(XK_K0 + rrow(r)) * XK_EPS;
+    for (int r = 0; r < 16; ++r) cx[r] = XK_BIAS + (float)(K0 + rrow(r)) * XK_EPS;
 
     const bool idle = c0_wave >= cols;  // wave-uniform; still joins the barriers
-    for (int base = 0; base < cols; base += chunk) {
+    const int nchunks = (cols + chunk - 1) / chunk;
+    // FREE: chunks downwards from the one holding the workgroup's highest col0
+    int cstart = 0;
+    if constexpr (FREE) cstart = min(cols - 1, (tile + 1) * waves * T * 32 - 1) / chunk;
+    int bprev = XK && !FREE ? -32 : 0;  // base of the previously reduced block
+    for (int k = 0; k < nchunks; ++k) {
+        int ci = FREE ? cstart - k : k;
+        if (ci < 0) ci += nchunks;
+        const int base = ci * chunk;
         const int ncols = min(chunk, cols - base);
-        if (base) __syncthreads();
+        if (k) __syncthreads();
         // expand the chunk's right descriptors: one col1 per thread, all its words
         for (int c = threadIdx.x; c < chunk; c += blockDim.x) {
             const int c1 = base + c;
@@ -230,10 +271,10 @@ void search_mx_kernel(SearchArgs a) {
                 uint32_t x = 0;
                 if (c1 < cols && w < WORDS) x = row1[(size_t)c1 * WORDS + w];
                 if (WORDS == 8 && w == 7) x &= 0x7FFFFFFFu;
-                const v4i e = expand_bits(x);
+                const v4i ex = expand_bits(x);
                 v4i v;
 #pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = e[q] << 1;  // 0x1 -> 0x2 (1.0)
+                for (int q = 0; q < 4; ++q) v[q] = ex[q] << 1;  // 0x1 -> 0x2 (1.0)
                 lds_mx[w * chunk + c] = v;
             }
         }
@@ -247,9 +288,11 @@ void search_mx_kernel(SearchArgs a) {
             cc = cx;
         } else {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) cc[r] = BIAS + (float)(base + rrow(r)) * EPS;
+            for (int r = 0; r < 16; ++r) cc[r] = KEY_BIAS + (float)(base + rrow(r)) * KEY_EPS;
         }
-        auto fragments = [&](int b, v4i* af, v4i* an) {
+        auto block = [&](int b, const v16f& c1, const v16f& c2) {
+            const int B = base + 32 * b;
+            v4i af[KS], an[KS];
 #pragma unroll
             for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + 32 * b + j];
             if constexpr (NODUPES && !XK) {
@@ -258,58 +301,56 @@ void search_mx_kernel(SearchArgs a) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) an[s][q] = af[s][q] | (af[s][q] << 2);  // 1.0 -> -1.0
             }
-        };
-        // C of a block reaching past the image: A = 0 there, so D1 = KEY_PAD, D2 = 0 never win
-        auto masked = [&](int b, v16f& c1, v16f& c2) {
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const bool in = 32 * b + rrow(r) < ncols;
-                c1[r] = in ? cc[r] : KEY_PAD;
-                c2[r] = in ? cc[r] : 0.f;
-            }
-        };
-        // one block: PIPE reduces tile t's previous block and issues its next products;
-        // otherwise products then keys, tile by tile (fewer live registers, more waves)
-        auto blockop = [&](int b, const v16f& c1, const v16f& c2, bool first) {
-            v4i af[KS], an[KS];
-            fragments(b, af, an);
+            // tile t+1's products are issued before tile t's keys are reduced, so the MFMAs
+            // overlap the reduction (and its branch) within the wave
+            products(0, af, an, c1, c2);
 #pragma unroll
             for (int t = 0; t < T; ++t) {
-                if constexpr (PIPE) {
-                    if (!first) reduce(t);
-                    products(t, af, an, c1, c2);
-                } else {
-                    products(t, af, an, c1, c2);
-                    reduce(t);
-                }
+                if (t + 1 < T) products(t + 1, af, an, c1, c2);
+                reduce(t, B, bprev);
             }
+            bprev = B;
         };
-        if (nfull == 0) {
+        // the block reaching past the image (last chunk): A = 0 there, so D1 = KEY_PAD,
+        // D2 = 0 never win. Ascending orders take it last, FREE first.
+        auto partial_block = [&](const v16f& cb) {
             v16f c1, c2;
-            masked(0, c1, c2);
-            blockop(0, c1, c2, true);
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const bool in = 32 * nfull + rrow(r) < ncols;
+                c1[r] = in ? cb[r] : KEY_PAD;
+                c2[r] = in ? cb[r] : 0.f;
+            }
+            block(nfull, c1, c2);
+        };
+        if constexpr (FREE) {
+            if (partial) partial_block(cc);
+            // full blocks downwards from the one holding the wave's highest col0 (clamped)
+            const int sb = max(0, min(nfull - 1, (c0_wave + 32 * T - 1 - base) / 32));
+            for (int i = 0; i < nfull; ++i) {
+                int b = sb - i;
+                if (b < 0) b += nfull;
+                block(b, cc, cc);
+            }
         } else {
-            blockop(0, cc, cc, true);
-        }
-        for (int b = 1; b < nfull; ++b) {
-            if constexpr (!XK) {
+            for (int b = 0; b < nfull; ++b) {
+                if constexpr (!XK) {
+                    if (b) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) cc[r] += 32.f * EPS;  // exact (same binade)
+                        for (int r = 0; r < 16; ++r) cc[r] += 32.f * KEY_EPS;  // exact (same binade)
+                    }
+                }
+                block(b, cc, cc);
             }
-            blockop(b, cc, cc, false);
-        }
-        if (partial && nfull > 0) {
-            if constexpr (!XK) {
+            if (partial) {
+                if constexpr (!XK) {
+                    if (nfull) {
 #pragma unroll
-                for (int r = 0; r < 16; ++r) cc[r] += 32.f * EPS;
+                        for (int r = 0; r < 16; ++r) cc[r] += 32.f * KEY_EPS;
+                    }
+                }
+                partial_block(cc);
             }
-            v16f c1, c2;
-            masked(nfull, c1, c2);
-            blockop(nfull, c1, c2, false);
-        }
-        if constexpr (PIPE) {
-#pragma unroll
-            for (int t = 0; t < T; ++t) reduce(t);
         }
     }
     if (idle) return;
@@ -317,18 +358,19 @@ void search_mx_kernel(SearchArgs a) {
     // the two lane halves hold the even / odd 4-row groups of every block
 #pragma unroll
     for (int t = 0; t < T; ++t) {
+        if constexpr (FREE) m2[t] += (uint32_t)(bprev - b2[t]);  // into the last block's frame
         m1[t] = min(m1[t], (uint32_t)__shfl_xor((int)m1[t], 32));
         if constexpr (NODUPES && XK) m2[t] = min(m2[t], (uint32_t)__shfl_xor((int)m2[t], 32));
         else if constexpr (NODUPES) m2[t] = max(m2[t], (uint32_t)__shfl_xor((int)m2[t], 32));
     }
     // best col1 of tile t, and whether it is the only column at the minimum cost
-    // XK: the minima are relative to the base of the last block
-    const int blast = ((cols + 31) & ~31) - 32;
+    // (XK: the minima are relative to the base of the last block reduced)
     auto best_of = [&](int t) {
-        return XK ? (int)(m1[t] & XK_COL) - XK_K0 + blast : key_col(m1[t]);
+        return XK ? (int)(m1[t] & XK_COL) - K0 + bprev : key_col(m1[t]);
     };
     auto unique_of = [&](int t, int best) {
-        if constexpr (NODUPES && XK) return 31 - (int)(m2[t] & XK_COL) + blast == best;
+        if constexpr (NODUPES && XK)
+            return (int)(XK_COL - K0) - (int)(m2[t] & XK_COL) + bprev == best;
         else if constexpr (NODUPES) return key_col(m2[t]) == best;
         return true;
     };
@@ -374,20 +416,19 @@ void search_mx_kernel(SearchArgs a) {
     }
 }
 
-template <int WORDS, bool NODUPES, int T, bool XK, bool PIPE>
+template <int WORDS, bool NODUPES, int T, int KEYS>
 hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     constexpr int WL = WORDS >= 2 ? WORDS : 2;
     const size_t lds = (size_t)WL * a.chunk * 16;
-    // fused agree only with the default NoDuplicates search (the pipeline's)
+    // fused agree only with the NoDuplicates search (the pipeline's)
     auto pick = [&]() {
-        if constexpr (NODUPES && !PIPE) {
-            if (a.out_f32) return a.depth == 2 ? search_mx_kernel<WORDS, NODUPES, T, XK, PIPE, 2>
-                                                : search_mx_kernel<WORDS, NODUPES, T, XK, PIPE, 1>;
+        if constexpr (NODUPES) {
+            if (a.out_f32) return a.depth == 2 ? search_mx_kernel<WORDS, NODUPES, T, KEYS, 2>
+                                               : search_mx_kernel<WORDS, NODUPES, T, KEYS, 1>;
         }
-        return search_mx_kernel<WORDS, NODUPES, T, XK, PIPE, 0>;
+        return search_mx_kernel<WORDS, NODUPES, T, KEYS, 0>;
     };
-    if (a.out_f32 && (!NODUPES || PIPE || (a.depth != 1 && a.depth != 2)))
-        return hipErrorInvalidValue;
+    if (a.out_f32 && (!NODUPES || (a.depth != 1 && a.depth != 2))) return hipErrorInvalidValue;
     const auto kern = pick();
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -398,44 +439,47 @@ hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     return hipGetLastError();
 }
 
-// Tile counts whose registers fit without scratch (checked with
-// -Rpass-analysis=kernel-resource-usage): 8 tiles only for 32/64-bit descriptors with one
-// key product (the pipeline keeps a 16-register D tile per tile live).
-constexpr bool mx_tiles_fit(int words, bool nodupes, bool xk, int t) {
-    return t <= 4 || (words == 1 && (xk || !nodupes)) || (words == 2 && !nodupes);
+// Tile counts whose registers fit (checked with -Rpass-analysis=kernel-resource-usage): 8
+// tiles only for 32/64-bit descriptors with one key product.
+constexpr bool mx_tiles_fit(int words, bool nodupes, int keys, int t) {
+    return t <= 4 || (words == 1 && (keys != 0 || !nodupes)) || (words == 2 && !nodupes);
 }
 
-template <int WORDS, bool NODUPES, bool XK, bool PIPE>
-hipError_t launch_mx_p(const SearchArgs& a, const MxGeometry& g, hipStream_t st) {
+template <int WORDS, bool NODUPES, int KEYS>
+hipError_t launch_mx_k(const SearchArgs& a, const MxGeometry& g, hipStream_t st) {
     if (g.T == 8) {
-        if constexpr (mx_tiles_fit(WORDS, NODUPES, XK, 8) && !PIPE) {
-            return launch_mx<WORDS, NODUPES, 8, XK, PIPE>(a, g.waves, st);
+        if constexpr (mx_tiles_fit(WORDS, NODUPES, KEYS, 8)) {
+            return launch_mx<WORDS, NODUPES, 8, KEYS>(a, g.waves, st);
         } else {  // does not fit: 4 tiles per wave, twice the workgroups per row
             SearchArgs b = a;
             const long per_wg = 32L * g.waves * 4;
             b.tiles_per_row = (int)((a.cols + per_wg - 1) / per_wg);
-            return launch_mx<WORDS, NODUPES, 4, XK, PIPE>(b, g.waves, st);
+            return launch_mx<WORDS, NODUPES, 4, KEYS>(b, g.waves, st);
         }
     }
     switch (g.T) {
-        case 2: return launch_mx<WORDS, NODUPES, 2, XK, PIPE>(a, g.waves, st);
-        case 4: return launch_mx<WORDS, NODUPES, 4, XK, PIPE>(a, g.waves, st);
+        case 2: return launch_mx<WORDS, NODUPES, 2, KEYS>(a, g.waves, st);
+        case 4: return launch_mx<WORDS, NODUPES, 4, KEYS>(a, g.waves, st);
     }
     return hipErrorInvalidValue;
 }
 
-template <int WORDS, bool NODUPES, bool XK>
-hipError_t launch_mx_k(const SearchArgs& a, const MxGeometry& g, hipStream_t st) {
-    return g.pipe ? launch_mx_p<WORDS, NODUPES, XK, true>(a, g, st)
-                  : launch_mx_p<WORDS, NODUPES, XK, false>(a, g, st);
-}
-
 template <int WORDS, bool NODUPES>
 hipError_t launch_mx_t(const SearchArgs& a, const MxGeometry& g, hipStream_t st) {
-    // without NoDuplicates both key forms are one product; the XK form also needs no
-    // float decode. The two-product form covers rows wider than 16384.
-    if (g.keys == 1 && a.cols <= 16384) return launch_mx_k<WORDS, NODUPES, true>(a, g, st);
-    return launch_mx_k<WORDS, NODUPES, false>(a, g, st);
+    // one-product XK keys by default: with NoDuplicates in any block order up to 8160
+    // columns (BICOS_MX_ORDER=natural: ascending), ascending up to 16384; the two-product
+    // float keys beyond that, or when tuned (variant 66)
+    static const bool natural = [] {
+        const char* v = std::getenv("BICOS_MX_ORDER");
+        return v && !std::strcmp(v, "natural");
+    }();
+    if (g.keys == 1) {
+        if constexpr (NODUPES) {
+            if (a.cols <= XKF_MAX_COLS && !natural) return launch_mx_k<WORDS, NODUPES, 2>(a, g, st);
+        }
+        if (a.cols <= 16384) return launch_mx_k<WORDS, NODUPES, 1>(a, g, st);
+    }
+    return launch_mx_k<WORDS, NODUPES, 0>(a, g, st);
 }
 
 template <int WORDS>
@@ -448,8 +492,7 @@ hipError_t launch_mx_w(const SearchArgs& a, const MxGeometry& g, bool nodupes, h
 MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int T, int waves,
                               int cus, int keys) {
     MxGeometry g;
-    g.keys = (keys & 3) == 2 ? 2 : 1;
-    g.pipe = (keys & 4) != 0;
+    g.keys = keys == 2 ? 2 : 1;
     const int wl = words >= 2 ? words : 2;
     // LDS chunk of expanded right descriptors (16 B per word per col1), multiple of 32
     int chunk = lds_bytes / (wl * 16);
@@ -461,10 +504,11 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     if (T) {
         g.T = T;
     } else {
-        // 4 tiles per wave (8 spill for most widths), 2 when the grid would not give every
-        // CU about two workgroups (narrow row bands)
+        // 4 tiles per wave (2 for 256-bit descriptors, whose 4-tile B fragments spill: cfg4
+        // 1.47 -> 1.09 ms, cfg4f 1.53 -> 0.64 ms; 8 spill for most widths), 2 when the grid
+        // would not give every CU about two workgroups (narrow row bands)
         g.T = 2;
-        for (int t = 4; t >= 2; t /= 2) {
+        for (int t = words >= 8 ? 2 : 4; t >= 2; t /= 2) {
             const long per_wg = 32L * g.waves * t;
             const long nwg = (long)rows * ((cols + per_wg - 1) / per_wg);
             if (nwg >= 2L * (cus > 0 ? cus : 256)) {

@@ -337,7 +337,7 @@ def test_fused_search_agree_equals_separate(gpu, n, H, W, dt, minvar):
     mv = None if minvar is None else float(np.float32(minvar) * np.float32(n))
     # default (matrix cores), VALU variants, matrix-core key forms / tile counts / pipeline
     for tune in [(0, 0, 0, 0), (16, 4, 8, 0), (16, 2, 8, 4), (65, 2, 8, 0), (65, 8, 4, 0),
-                 (66, 4, 8, 0), (69, 4, 8, 0)]:
+                 (66, 4, 8, 0), (64, 4, 8, 40)]:
         gpu.tune(*tune)
         try:
             fo, fc = gpu.search_agree(d0, d1, s0, s1, words, 0.8, minvar_scaled=mv)
@@ -447,7 +447,7 @@ def test_search_tuning_settings_are_exact(gpu, oracle, words):
 # all-one right descriptors), rows that are not a multiple of the 32-column block, rows
 # wider than one LDS chunk, every tile count -- against the oracle and the VALU search.
 @pytest.mark.parametrize("words", [1, 2, 4, 8])
-@pytest.mark.parametrize("W", [1, 31, 33, 95, 2049, 4111, 16385])
+@pytest.mark.parametrize("W", [1, 31, 33, 95, 2049, 4111, 8161, 16385])
 def test_mx_search_edges(gpu, oracle, words, W):
     H = 3
     rng = np.random.default_rng(W * 10 + words)

@@ -54,6 +54,10 @@ for step in "$@"; do
         bench5) run bench5 600 python bench.py --config cfg5 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
         sweepv) run sweepv_${SC:-cfg2}_${SROWS:-all} 600 python tools/search_sweep.py --config ${SC:-cfg2} ${SROWS:+--rows $SROWS} --variants $SV ;;
         pmcmx) run pmcmx 120 timeout -s KILL 100 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d gpurun_out/pmcmx -o run --output-format csv -- python tools/search_sweep.py --rounds 1 --reps 2 --variants ${SV:-64:8:8} ;;
+        pmcclk) for c in ${CLKCFG:-cfg2 cfg4}; do
+                run pmcclk_$c 120 timeout -s KILL 100 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU -d gpurun_out/pmcclk_$c -o run --output-format csv -- python tools/search_sweep.py --config $c --rounds 1 --reps 3 --variants ${SV:-0:0:0}
+            done ;;
+        sweepnat) BICOS_MX_ORDER=natural run sweepnat_${SC:-cfg2} 600 python tools/search_sweep.py --config ${SC:-cfg2} --variants $SV ;;
         sweep) run sweep 600 python tools/search_sweep.py --variants 16:2:8:2,18:2:8:2,16:2:8:1,18:2:8:1,18:4:8:2,17:2:8:2 ;;
         sweep4) run sweep4 600 python tools/search_sweep.py --config cfg4 --variants 16:2:8:2,18:2:8:2,18:4:8:2 ;;
         sweep1) run sweep1 600 python tools/search_sweep.py --config cfg1 --variants 32:1:4,32:2:4,16:2:4,16:4:4,16:2:2,16:2:1 ;;
