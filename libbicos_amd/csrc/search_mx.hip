@@ -228,6 +228,15 @@ void search_mx_kernel(SearchArgs a) {
     // block at base B, the previous one at base bp (XK: the running minima move from bp's
     // frame to B's first)
     auto reduce = [&](int t, int B, int bp) {
+#if defined(BICOS_MX_DIAG)  // diagnostic builds only (tools/build_diag.sh): results are wrong
+        if constexpr (BICOS_MX_DIAG == 1) {  // MFMA skeleton: one key per tile
+            m1[t] = min(m1[t], fbits(d[t][0]));
+            return;
+        } else if constexpr (BICOS_MX_DIAG == 2) {  // + the first-minimum tree only
+            m1[t] = min16(d[t], m1[t], 0u);
+            return;
+        }
+#endif
         if constexpr (FREE) {
             const uint32_t m1s = m1[t] - (uint32_t)(B - bp);
             const uint32_t bm = min16(d[t], 0xFFFFFFFFu, 0u);   // this half's block minimum
@@ -400,10 +409,15 @@ void search_mx_kernel(SearchArgs a) {
         return;
     }
     int16_t* out = a.out + (size_t)row * a.out_pitch;
+    // (lane index made opaque: otherwise the compiler hoists these addresses into the
+    // prologue, where they share c0 with the B-fragment loads, and spills them to scratch
+    // across the whole search -- 68 MB of scratch writes per cfg2 launch)
+    int jo = j;
+    asm volatile("" : "+v"(jo));
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         if ((t & 1) != h) continue;  // half 0 writes even tiles, half 1 odd tiles
-        const int c0 = c0_wave + 32 * t + j;
+        const int c0 = c0_wave + 32 * t + jo;
         if (c0 >= cols) continue;
         const int best = best_of(t);
         const bool ok = unique_of(t, best);

@@ -58,6 +58,14 @@ for step in "$@"; do
                 run pmcclk_$c 120 timeout -s KILL 100 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU -d gpurun_out/pmcclk_$c -o run --output-format csv -- python tools/search_sweep.py --config $c --rounds 1 --reps 3 --variants ${SV:-0:0:0}
             done ;;
         sweepnat) BICOS_MX_ORDER=natural run sweepnat_${SC:-cfg2} 600 python tools/search_sweep.py --config ${SC:-cfg2} --variants $SV ;;
+        diag)  # search-kernel floors: diagnostic builds (tools/build_diag.sh) vs the real one
+            cp libbicos_amd/libbicos_amd.so build/cur.so
+            run diag_real_${SC:-cfg2} 300 python tools/search_sweep.py --config ${SC:-cfg2} --variants ${SV:-0:0:0}
+            for d in 1 2; do
+                cp build/diag$d.so libbicos_amd/libbicos_amd.so
+                run diag${d}_${SC:-cfg2} 300 python tools/search_sweep.py --config ${SC:-cfg2} --variants ${SV:-0:0:0}
+            done
+            cp build/cur.so libbicos_amd/libbicos_amd.so ;;
         sweep) run sweep 600 python tools/search_sweep.py --variants 16:2:8:2,18:2:8:2,16:2:8:1,18:2:8:1,18:4:8:2,17:2:8:2 ;;
         sweep4) run sweep4 600 python tools/search_sweep.py --config cfg4 --variants 16:2:8:2,18:2:8:2,18:4:8:2 ;;
         sweep1) run sweep1 600 python tools/search_sweep.py --config cfg1 --variants 32:1:4,32:2:4,16:2:4,16:4:4,16:2:2,16:2:1 ;;
