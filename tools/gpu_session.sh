@@ -61,7 +61,7 @@ for step in "$@"; do
         diag)  # search-kernel floors: diagnostic builds (tools/build_diag.sh) vs the real one
             cp libbicos_amd/libbicos_amd.so build/cur.so
             run diag_real_${SC:-cfg2} 300 python tools/search_sweep.py --config ${SC:-cfg2} --variants ${SV:-0:0:0}
-            for d in 1 2; do
+            for d in 1 2 3; do
                 cp build/diag$d.so libbicos_amd/libbicos_amd.so
                 run diag${d}_${SC:-cfg2} 300 python tools/search_sweep.py --config ${SC:-cfg2} --variants ${SV:-0:0:0}
             done
