@@ -16,6 +16,8 @@ run() {  # name timeout cmd...
 for step in "$@"; do
     case $step in
         valu) run valu 120 ./build/valu_peak ;;
+        mfma) run mfma 200 ./build/mfma_rate ;;
+        planeread) run planeread 120 ./build/plane_read ;;
         dep) run dep 200 ./build/dep_bench ;;
         smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
         pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
@@ -43,6 +45,7 @@ for step in "$@"; do
             for th in ${HOST_THREADS:-4 8 16}; do
                 BICOS_HOST_THREADS=$th run hostk_${th} 300 python tools/host_bench.py --reps 7
             done ;;
+        pytestsub) run pytest_sub 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "subpix or cfg3 or match_bit_exact" ;;
         subpix16) run subpix16 300 python tools/subpix_bench.py --depth 2 --ns 8,16,24,33 ;;
         bench4) run bench4 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
         bench4tp) BICOS_CONSISTENCY=twopass run bench4tp 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
