@@ -21,6 +21,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
+#include <cstring>
+
 #include <type_traits>
 
 namespace bicos_hip {
@@ -1129,44 +1132,147 @@ __global__ __launch_bounds__(256) void agree_reg_kernel(AgreeArgs a) {
     if (col >= a.cols) return;
     const size_t o = (size_t)row * a.cols + col;
     int d = a.raw[(size_t)row * a.raw_pitch + col];
-    TPrec corr = (TPrec)__builtin_nan("");
-    if (d != INVALID_I16) {
-        const int idx1 = col - d;
-        if (idx1 < 0 || idx1 >= a.cols) {
-            d = INVALID_I16;
-        } else {
-            const int n = EXACT ? MAXN : a.n;
-            const size_t pp = a.plane_pitch;
-            const StackReader<TIn> rd0(a.stack0, a.stack_bytes), rd1(a.stack1, a.stack_bytes);
-            const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
-            uint32_t l[MAXN], r[MAXN];
-            uint32_t sl = 0, sr = 0;
+    // Straight-line loads: the left samples do not depend on d, so they are issued while
+    // the disparity load is in flight; the right ones read column col for pixels without
+    // a match (cached, discarded). Branching on d first serialised the two loads per wave
+    // (the kernel was latency-bound at 3.2 TB/s; a plain planar read runs at 6.8).
+    const int idx1 = col - d;
+    const bool inb = d != INVALID_I16 && idx1 >= 0 && idx1 < a.cols;
+    const int n = EXACT ? MAXN : a.n;
+    const size_t pp = a.plane_pitch;
+    const StackReader<TIn> rd0(a.stack0, a.stack_bytes), rd1(a.stack1, a.stack_bytes);
+    const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
+    uint32_t l[MAXN], r[MAXN];
+    uint32_t sl = 0, sr = 0;
 #pragma unroll
-            for (int t = 0; t < MAXN; ++t)
-                if (t < n) {
-                    l[t] = rd0((uint32_t)col, rowoff + (uint32_t)(t * pp));
-                    r[t] = rd1((uint32_t)idx1, rowoff + (uint32_t)(t * pp));
-                    sl += l[t];
-                    sr += r[t];
-                }
-            const TPrec m0 = div_p((TPrec)sl, (TPrec)n);
-            const TPrec m1 = div_p((TPrec)sr, (TPrec)n);
-            TPrec cov = 0, v0 = 0, v1 = 0;
+    for (int t = 0; t < MAXN; ++t)
+        if (t < n) l[t] = rd0((uint32_t)col, rowoff + (uint32_t)(t * pp));
+    const uint32_t c1 = inb ? (uint32_t)idx1 : (uint32_t)col;
 #pragma unroll
-            for (int t = 0; t < MAXN; ++t)
-                if (t < n) {
-                    const TPrec x0 = (TPrec)l[t] - m0;
-                    const TPrec x1 = (TPrec)r[t] - m1;
-                    cov = fma_p(x0, x1, cov);
-                    v0 = fma_p(x0, x0, v0);
-                    v1 = fma_p(x1, x1, v1);
-                }
-            if (a.has_minvar && (v0 < (TPrec)a.minvar || v1 < (TPrec)a.minvar))
-                corr = (TPrec)-1;
-            else
-                corr = div_p(cov, sqrt_p(v0 * v1));
-            if (corr < (TPrec)a.threshold) d = INVALID_I16;  // NaN passes, as in the reference
+    for (int t = 0; t < MAXN; ++t)
+        if (t < n) r[t] = rd1(c1, rowoff + (uint32_t)(t * pp));
+#pragma unroll
+    for (int t = 0; t < MAXN; ++t)
+        if (t < n) {
+            sl += l[t];
+            sr += r[t];
         }
+    TPrec corr = (TPrec)__builtin_nan("");
+    if (inb) {
+        const TPrec m0 = div_p((TPrec)sl, (TPrec)n);
+        const TPrec m1 = div_p((TPrec)sr, (TPrec)n);
+        TPrec cov = 0, v0 = 0, v1 = 0;
+#pragma unroll
+        for (int t = 0; t < MAXN; ++t)
+            if (t < n) {
+                const TPrec x0 = (TPrec)l[t] - m0;
+                const TPrec x1 = (TPrec)r[t] - m1;
+                cov = fma_p(x0, x1, cov);
+                v0 = fma_p(x0, x0, v0);
+                v1 = fma_p(x1, x1, v1);
+            }
+        if (a.has_minvar && (v0 < (TPrec)a.minvar || v1 < (TPrec)a.minvar))
+            corr = (TPrec)-1;
+        else
+            corr = div_p(cov, sqrt_p(v0 * v1));
+        if (corr < (TPrec)a.threshold) d = INVALID_I16;  // NaN passes, as in the reference
+    } else {
+        d = INVALID_I16;
+    }
+    if (a.out_f32)
+        ((float*)a.out)[o] = (float)d;
+    else
+        ((int16_t*)a.out)[o] = (int16_t)d;
+    if (a.corrmap) ((TPrec*)a.corrmap)[o] = corr;
+}
+
+// agree_reg_kernel with the left samples staged through LDS: the workgroup's 256-column
+// tile of all n left planes is fetched with dword loads (one wave-uniform plane per load:
+// 64 lanes x 4 B = one 256-byte plane row of 8-bit data), so a lane keeps only its n right
+// samples in registers (~55 VGPRs at n = 33: 8 waves/SIMD instead of 4). The right
+// samples are gathered at col - d as before; the left loads, the disparity load and the
+// right gathers are all in flight together. Requires 4-byte aligned stacks, row and
+// plane pitches (checked on the host; agree_reg_kernel otherwise). Same contract and
+// results as agree_reg_kernel.
+template <typename TIn, typename TPrec, int MAXN, bool EXACT>
+__global__ __launch_bounds__(256) void agree_lds_kernel(AgreeArgs a) {
+    constexpr int DW = 64 * (int)sizeof(TIn);  // dwords per plane of a 256-column tile
+    constexpr int WPP = 256 / DW;              // planes per pass of the workgroup
+    constexpr int PASSES = (MAXN + WPP - 1) / WPP;
+    __shared__ uint32_t tile_l[MAXN * DW];
+    int tile, row;
+    xcd_rows(tile, row);
+    const int col0 = tile * 256;
+    const int col = col0 + (int)threadIdx.x;
+    const bool live = col < a.cols;
+    const int n = EXACT ? MAXN : a.n;
+    const uint32_t pp = (uint32_t)a.plane_pitch;
+    const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
+    int d = live ? (int)a.raw[(size_t)row * a.raw_pitch + col] : INVALID_I16;
+    const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(a.stack0), (short)0, (int)a.stack_bytes, 0x00020000);
+    // left tile loads: pass j, wave-uniform plane p = j * WPP + tid / DW, dword tid % DW
+    const int p0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x / DW);
+    const uint32_t lane_b = (uint32_t)col0 * sizeof(TIn) + 4u * (threadIdx.x % DW);
+    uint32_t w[PASSES];
+#pragma unroll
+    for (int j = 0; j < PASSES; ++j) {
+        // unconditional (planes past n re-read plane n-1, not stored): a guarded load
+        // ends in a control-flow join where the waitcnt pass waits for every load
+        const int p = min(j * WPP + p0, n - 1);
+        w[j] = __builtin_amdgcn_raw_buffer_load_b32(
+            r0, lane_b, (rowoff + (uint32_t)p * pp) * (uint32_t)sizeof(TIn), 0);
+    }
+    const int idx1 = col - d;
+    const bool inb = live && d != INVALID_I16 && idx1 >= 0 && idx1 < a.cols;
+    const uint32_t c1 = inb ? (uint32_t)idx1 : 0u;
+    const StackReader<TIn> rd1(a.stack1, a.stack_bytes);
+    uint32_t r[MAXN];
+#pragma unroll
+    for (int t = 0; t < MAXN; ++t)  // unconditional as above (slots past n: plane n-1)
+        r[t] = rd1(c1, rowoff + (uint32_t)min(t, n - 1) * pp);
+#pragma unroll
+    for (int j = 0; j < PASSES; ++j) {
+        const int p = j * WPP + p0;
+        if (p < n) tile_l[p * DW + threadIdx.x % DW] = w[j];
+    }
+    __syncthreads();
+    if (!live) return;
+    const TIn* lt = (const TIn*)tile_l + threadIdx.x;  // plane t at lt[t * 256]
+    const size_t o = (size_t)row * a.cols + col;
+    TPrec corr = (TPrec)__builtin_nan("");
+    if (inb) {
+        uint32_t sl = 0, sr = 0;
+#pragma unroll
+        for (int t = 0; t < MAXN; ++t)
+            if (t < n) {
+                sl += lt[t * 256];
+                sr += r[t];
+                // LDS reads next to their use: hoisted, they cost n more VGPRs
+                if ((t & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+            }
+        // re-read the left samples from LDS in the second pass instead of holding them
+        asm volatile("" ::: "memory");
+        const TPrec m0 = div_p((TPrec)sl, (TPrec)n);
+        const TPrec m1 = div_p((TPrec)sr, (TPrec)n);
+        TPrec cov = 0, v0 = 0, v1 = 0;
+#pragma unroll
+        for (int t = 0; t < MAXN; ++t)
+            if (t < n) {
+                const TPrec x0 = (TPrec)(uint32_t)lt[t * 256] - m0;
+                const TPrec x1 = (TPrec)r[t] - m1;
+                cov = fma_p(x0, x1, cov);
+                v0 = fma_p(x0, x0, v0);
+                v1 = fma_p(x1, x1, v1);
+                if ((t & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+            }
+        if (a.has_minvar && (v0 < (TPrec)a.minvar || v1 < (TPrec)a.minvar))
+            corr = (TPrec)-1;
+        else
+            corr = div_p(cov, sqrt_p(v0 * v1));
+        if (corr < (TPrec)a.threshold) d = INVALID_I16;  // NaN passes, as in the reference
+    } else {
+        d = INVALID_I16;
     }
     if (a.out_f32)
         ((float*)a.out)[o] = (float)d;
@@ -1492,6 +1598,20 @@ hipError_t launch_subpixel_t(const AgreeArgs& a, hipStream_t st) {
 template <typename TIn, typename TPrec, int MAXN>
 hipError_t launch_agree_m(const AgreeArgs& a, hipStream_t st) {
     dim3 grid((a.cols + 255) / 256, a.rows);
+    // left tile through LDS when the dword loads are aligned (BICOS_AGREE=reg: never)
+    static const bool reg_env = [] {
+        const char* v = std::getenv("BICOS_AGREE");
+        return v && !std::strcmp(v, "reg");
+    }();
+    const size_t sz = sizeof(TIn);
+    const bool aligned = ((uintptr_t)a.stack0 % 4 == 0) && (a.row_pitch * sz) % 4 == 0 &&
+                         (a.plane_pitch * sz) % 4 == 0;
+    if (aligned && !reg_env) {
+        // runtime n even for an exact bucket: with a constant n the compiler front-loads
+        // the conversions and doubles the VGPRs (49 -> 100 at n = 33)
+        hipLaunchKernelGGL((agree_lds_kernel<TIn, TPrec, MAXN, false>), grid, dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     if (a.n == MAXN)
         hipLaunchKernelGGL((agree_reg_kernel<TIn, TPrec, MAXN, true>), grid, dim3(256), 0, st, a);
     else

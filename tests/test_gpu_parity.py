@@ -119,8 +119,9 @@ def test_search_multi_chunk(gpu, oracle):
 @pytest.mark.parametrize("n,dt", [(2, np.uint8), (8, np.uint8), (33, np.uint8), (17, np.uint16),
                                   (40, np.uint8), (65, np.uint8)])
 @pytest.mark.parametrize("minvar", [None, 2.0])
-def test_agree_bit_exact(gpu, oracle, n, dt, minvar):
-    H, W = 9, 200
+@pytest.mark.parametrize("W", [200, 203, 600])  # 4-byte aligned pitches: LDS-staged kernel
+def test_agree_bit_exact(gpu, oracle, n, dt, minvar, W):
+    H = 9
     L, R = stereo_stack(n, H, W, dt, dmin=3, drange=20, seed=n)
     rng = np.random.default_rng(n)
     raw = rng.integers(-5, 30, size=(H, W)).astype(np.int16)

@@ -46,6 +46,15 @@ for step in "$@"; do
                 BICOS_HOST_THREADS=$th run hostk_${th} 300 python tools/host_bench.py --reps 7
             done ;;
         pytestsub) run pytest_sub 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "subpix or cfg3 or match_bit_exact" ;;
+        abag)  # agree/subpixel stages alone: current lib vs build/alt.so, interleaved twice
+            cp libbicos_amd/libbicos_amd.so build/cur.so
+            for k in 1 2; do
+                cp build/cur.so libbicos_amd/libbicos_amd.so
+                run abag_cur$k 300 python tools/subpix_bench.py --ns ${AGNS:-33,40,16} --rows 1536
+                cp build/alt.so libbicos_amd/libbicos_amd.so
+                run abag_alt$k 300 python tools/subpix_bench.py --ns ${AGNS:-33,40,16} --rows 1536
+            done
+            cp build/cur.so libbicos_amd/libbicos_amd.so ;;
         subpix16) run subpix16 300 python tools/subpix_bench.py --depth 2 --ns 8,16,24,33 ;;
         bench4) run bench4 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
         bench4tp) BICOS_CONSISTENCY=twopass run bench4tp 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
