@@ -240,10 +240,18 @@ void search_mx_kernel(SearchArgs a) {
         if constexpr (FREE) {
             const uint32_t m1s = m1[t] - (uint32_t)(B - bp);
             const uint32_t bm = min16(d[t], 0xFFFFFFFFu, 0u);   // this half's block minimum
+#if defined(BICOS_MX_DIAG) && BICOS_MX_DIAG == 4  // timing only: the last-minimum path never runs
+            const bool reach = bm <= (m1s | XK_COL) && bm == 0u;
+#else
             const bool reach = bm <= (m1s | XK_COL);           // cost <= running minimum cost
+#endif
             const auto sw = __builtin_amdgcn_permlane32_swap(bm, bm, false, false);
             m1[t] = umin3(m1s, sw[0], sw[1]);                  // both halves' minimum
+#if defined(BICOS_MX_DIAG) && BICOS_MX_DIAG == 5  // timing only: no last-minimum branch at all
+            if (false) {
+#else
             if (__builtin_amdgcn_ballot_w64(reach)) {
+#endif
                 m2[t] = min16(d[t], m2[t] + (uint32_t)(B - b2[t]), XK_COL);
                 b2[t] = B;
             }
@@ -271,9 +279,14 @@ void search_mx_kernel(SearchArgs a) {
         if (ci < 0) ci += nchunks;
         const int base = ci * chunk;
         const int ncols = min(chunk, cols - base);
-        if (k) __syncthreads();
+#if defined(BICOS_MX_DIAG) && BICOS_MX_DIAG == 3  // timing only: expand the first chunk only
+        const bool expand = k == 0;
+#else
+        constexpr bool expand = true;
+#endif
+        if (k && expand) __syncthreads();
         // expand the chunk's right descriptors: one col1 per thread, all its words
-        for (int c = threadIdx.x; c < chunk; c += blockDim.x) {
+        for (int c = threadIdx.x; expand && c < chunk; c += blockDim.x) {
             const int c1 = base + c;
 #pragma unroll
             for (int w = 0; w < WL; ++w) {
@@ -287,7 +300,7 @@ void search_mx_kernel(SearchArgs a) {
                 lds_mx[w * chunk + c] = v;
             }
         }
-        __syncthreads();
+        if (expand) __syncthreads();
         if (idle) continue;
 
         const int nfull = ncols / 32;

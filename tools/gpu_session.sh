@@ -47,6 +47,24 @@ for step in "$@"; do
                 BICOS_HOST_THREADS=$th run hostk_${th} 300 python tools/host_bench.py --reps 7
             done ;;
         pytestsub) run pytest_sub 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "subpix or cfg3 or match_bit_exact" ;;
+        absearch)  # search kernel alone: current lib vs build/alt.so, interleaved twice
+            cp libbicos_amd/libbicos_amd.so build/cur.so
+            for k in 1 2; do
+                cp build/cur.so libbicos_amd/libbicos_amd.so
+                run absearch_cur${k}_${SC:-cfg2} 300 python tools/search_sweep.py --config ${SC:-cfg2} --variants 0:0:0
+                cp build/alt.so libbicos_amd/libbicos_amd.so
+                run absearch_alt${k}_${SC:-cfg2} 300 python tools/search_sweep.py --config ${SC:-cfg2} --variants 0:0:0
+            done
+            cp build/cur.so libbicos_amd/libbicos_amd.so ;;
+        abn)  # search kernel alone over several builds (LIBS="alt share2 ..." = build/<x>.so), interleaved twice
+            cp libbicos_amd/libbicos_amd.so build/cur.so
+            for k in 1 2; do
+                for l in ${LIBS}; do
+                    cp build/$l.so libbicos_amd/libbicos_amd.so
+                    run abn_${l}_${k}_${SC:-cfg2} 300 python tools/search_sweep.py --config ${SC:-cfg2} --variants 0:0:0
+                done
+            done
+            cp build/cur.so libbicos_amd/libbicos_amd.so ;;
         abag)  # agree/subpixel stages alone: current lib vs build/alt.so, interleaved twice
             cp libbicos_amd/libbicos_amd.so build/cur.so
             for k in 1 2; do
@@ -74,7 +92,7 @@ for step in "$@"; do
         diag)  # search-kernel floors: diagnostic builds (tools/build_diag.sh) vs the real one
             cp libbicos_amd/libbicos_amd.so build/cur.so
             run diag_real_${SC:-cfg2} 300 python tools/search_sweep.py --config ${SC:-cfg2} --variants ${SV:-0:0:0}
-            for d in 1 2 3; do
+            for d in ${DIAGS:-1 2 3}; do
                 cp build/diag$d.so libbicos_amd/libbicos_amd.so
                 run diag${d}_${SC:-cfg2} 300 python tools/search_sweep.py --config ${SC:-cfg2} --variants ${SV:-0:0:0}
             done
