@@ -18,6 +18,7 @@ for step in "$@"; do
         valu) run valu 120 ./build/valu_peak ;;
         mfma) run mfma 200 ./build/mfma_rate ;;
         bands) run bands 300 python tools/band_bench.py --config ${SC:-cfg2} ;;
+        hostov) run hostov 300 python tools/host_overhead.py ;;
         planeread) run planeread 120 ./build/plane_read ;;
         dep) run dep 200 ./build/dep_bench ;;
         smoke) run smoke 400 python -c "import __graft_entry__ as g; g.smoke()" ;;
