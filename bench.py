@@ -46,6 +46,9 @@ VALU_NOMINAL_TOPS = 256 * 128 * 2.4e9 / 1e12   # 78.6: every op at full rate, 2.
 # Dense FP4 MFMA peak (MI355X_MICROARCH.md "Peak FP6/FP4 MFMA": ~10 PF dense, the 20 PF
 # figure is 2:1 sparsity): v_mfma_scale_f32_32x32x64_f8f6f4 on FP4 operands.
 MFMA_FP4_DENSE_TFLOPS = 10000.0
+# sustained v_mfma_scale_f32_32x32x64_f8f6f4 (FP4) rate measured on the box, 4 waves/SIMD
+# (tools/mfma_rate.hip, profiles/mfma_rates_r01.jsonl): the clock the pipe actually runs at
+MFMA_FP4_SUSTAINED_TFLOPS = 8360.0
 
 CONFIGS = {
     # BASELINE.json configs; "cfg2" is the one the headline metric is quoted on
@@ -376,6 +379,11 @@ def main():
             "ms_per_launch": round(t_search * 1e3, 4),
             "peak_model": "dense FP4 MFMA peak (MI355X_MICROARCH.md); algorithmic FLOPs = "
                           "2 x descriptor bits per Hamming pair",
+            "sustained_view": {
+                "peak": MFMA_FP4_SUSTAINED_TFLOPS,
+                "frac": round(achieved_tf / MFMA_FP4_SUSTAINED_TFLOPS, 4),
+                "source": "profiles/mfma_rates_r01.jsonl (tools/mfma_rate.hip, 4 waves/SIMD)",
+            },
             "valu_view": {
                 "what": "the VALU key reduction (v_min3 + v_xor per pair) that bounds the "
                         "kernel; issue bound at the measured rates, see DESIGN.md s5",

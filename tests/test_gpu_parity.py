@@ -161,6 +161,26 @@ def test_subpixel_bit_exact(gpu, oracle, n, dt, step, minvar):
     same(host(corr), rc)
 
 
+# Subpixel over several tiles per row with mixed rows: matches spread over 500 columns,
+# rows without a valid match, matches on both edge columns, padded buckets.
+@pytest.mark.parametrize("n,dt", [(8, np.uint8), (16, np.uint8), (25, np.uint8), (33, np.uint8),
+                                  (12, np.uint16), (24, np.uint16), (33, np.uint16)])
+def test_subpixel_mixed_rows(gpu, oracle, n, dt):
+    H, W = 24, 512
+    L = random_stack(n, H, W, dt, seed=3 * n + 1)
+    R = random_stack(n, H, W, dt, seed=3 * n + 2)
+    rng = np.random.default_rng(n + 100)
+    raw = rng.integers(-3, 40, size=(H, W)).astype(np.int16)
+    raw[3] = rng.integers(0, 500, size=W)       # matches spread over the whole row
+    raw[5] = -32768                              # no match in the row
+    raw[7, :] = np.arange(W) - (np.arange(W) % 2) * (W - 1)  # col1 = 0 / W-1 edges
+    raw[rng.random((H, W)) < 0.1] = -32768
+    ro, rc = oracle.agree_subpixel(raw, L, R, 0.2, 0.1, None)
+    out, corr = gpu.agree(dev(raw), dev(L), dev(R), 0.2, None, step=0.1)
+    same(host(out), ro)
+    same(host(corr), rc)
+
+
 # Narrow images and every col1 (0, 1, interior, cols-2, cols-1): the subpixel kernel reads
 # the right neighbours with one window load except below 4 columns (byte loads).
 @pytest.mark.parametrize("W", [3, 4, 5, 9])

@@ -17,6 +17,9 @@ for step in "$@"; do
     case $step in
         valu) run valu 120 ./build/valu_peak ;;
         mfma) run mfma 200 ./build/mfma_rate ;;
+        sweepband)  # geometry candidates for narrow row bands (N=8: 192 rows, N=4: 384)
+            run sweepband192 300 python tools/search_sweep.py --rows 192 --variants ${SV192:-0:0:0,64:4:8:0,64:2:8:0,64:4:4:32,64:2:4:32,64:4:8:48}
+            run sweepband384 300 python tools/search_sweep.py --rows 384 --variants ${SV384:-0:0:0,64:4:8:0,64:2:8:0,64:4:4:32,64:4:8:48} ;;
         bands) run bands 300 python tools/band_bench.py --config ${SC:-cfg2} ;;
         hostov) run hostov 300 python tools/host_overhead.py ;;
         planeread) run planeread 120 ./build/plane_read ;;
