@@ -20,8 +20,9 @@ Extra keys on the JSON line:
                 binds it. BICOS_SEARCH=valu: pairs/s vs the VALU
                 issue bound of the popcount search. `hbm` holds the HBM-bound stages
                 (transform, agree) against the 8 TB/s peak.
-  cpu_baseline  the C oracle (oracle/bicos_oracle.c, -march=x86-64-v3) on this
-                host's cores, rank 0 at N=1 only, over a bounded row sample.
+  cpu_baseline  the C oracle (oracle/bicos_oracle.c, -march=x86-64-v3; the as-shipped
+                -O3 build beside it) on every host core this process may use, rank 0
+                at N=1 only, over a bounded row sample (CPU model / nproc stated).
 """
 from __future__ import annotations
 
@@ -149,6 +150,42 @@ def load_traffic(kernel_prefix: str, rows: int, W: int):
     return None
 
 
+def launch_ranks(world: int) -> int:
+    """One child process per rank (what torchrun would start): RANK / LOCAL_RANK /
+    WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free MASTER_PORT in the environment, the same
+    argv. Rank 0 prints the JSON line (the children share our stdout); the other ranks print
+    nothing. Returns the first non-zero exit status, else 0. A rank that fails takes the
+    others down (they would block in the next collective)."""
+    import signal
+    import socket
+    import subprocess
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
+                   LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                      env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 128 - code
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+        if live:
+            time.sleep(0.05)
+    return rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -165,14 +202,39 @@ def main():
     ap.add_argument("--kernel-reps", type=int, default=10)
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the end-to-end host-buffer measurement (rank 0, N=1)")
+    ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo = rehearsal of the N>1 "
                          "path with several ranks sharing one GPU (not a measurement)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without torchrun: start the N ranks ourselves, before
+        # this process touches torch or HIP (no exec from a GPU-initialised process)
+        raise SystemExit(launch_ranks(args.gpus))
 
     import numpy as np
     import torch
     import torch.distributed as dist
+
+    if args.selftest_launch:
+        # launcher check without a GPU (tests/test_bench_launch.py): the ranks rendezvous
+        # over gloo exactly as the bench does and rank 0 reports what it saw
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        rank = int(os.environ.get("RANK", "0"))
+        if os.environ.get("BICOS_SELFTEST_FAIL_RANK") == str(rank):
+            raise SystemExit(3)
+        if world > 1:
+            dist.init_process_group("gloo")
+        t = torch.tensor([rank + 1.0])
+        if world > 1:
+            dist.all_reduce(t)
+        if rank == 0:
+            print(json.dumps({"selftest": "launch", "world": world, "gpus": args.gpus,
+                              "rank_sum": float(t.item()),
+                              "pid_parent": os.getppid()}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     from libbicos_amd import _lib, device
     from libbicos_amd.distributed import band_height, band_rows
@@ -511,41 +573,90 @@ def host_path(C, mcfg, reps):
     }
 
 
+def host_cpu_info():
+    """CPU model, logical CPUs of the machine (nproc), CPUs this process may run on
+    (affinity) and the cgroup CPU quota in cores (None when unlimited)."""
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count() or 1
+    return {"model": model, "nproc": os.cpu_count(), "affinity": affinity, "cgroup_quota": quota}
+
+
 def cpu_baseline(C, seconds):
-    """The C oracle on this host's cores over a bounded row sample of the same frame."""
+    """The C oracle (a restatement of the reference CPU path, oracle/bicos_oracle.c) on every
+    host core this process may use, over a bounded row sample of the same frame: the x86-64-v3
+    build (popcnt/AVX2) is `value`; the as-shipped-flags build (-O3, no -march: libgcc
+    popcount, like the reference's CMake build) is timed on the same sample beside it. Rows
+    are independent (SURVEY.md s8 e), so the per-frame rate is the sample's rows/s x cols."""
     import numpy as np
     from libbicos_amd.synthetic import stereo_stack
     from oracle import oracle
 
     n, H, W = C["n"], C["H"], C["W"]
-    cores = min(os.cpu_count() or 1, 16)
+    info = host_cpu_info()
+    cores = info["affinity"]
+    if info["cgroup_quota"]:
+        cores = max(1, min(cores, int(info["cgroup_quota"])))
     ocfg = oracle.OracleConfig(**C["cfg"])
     probe = max(cores, 8)
     L, R = stereo_stack(n, H, W, np.uint8, row_begin=0, row_end=probe)
     t = time.perf_counter()
     oracle.match(L, R, ocfg, nthreads=cores, variant="v3")
     per_row = (time.perf_counter() - t) / probe
-    # `seconds` of CPU time in all (wall = seconds / cores): a row sample of the frame, or
+    # `seconds` of CPU time per build (wall = seconds / cores): a row sample of the frame, or
     # whole frames repeated when one frame takes less than that
     wall = seconds / cores
     rows = int(max(probe, min(H, wall / max(per_row, 1e-9))))
-    rows = max(cores, rows // cores * cores)
+    rows = min(H, max(cores, rows // cores * cores))
     L, R = stereo_stack(n, H, W, np.uint8, row_begin=0, row_end=rows)
-    reps, el = 0, 0.0
-    while reps == 0 or el < wall:
-        t = time.perf_counter()
-        oracle.match(L, R, ocfg, nthreads=cores, variant="v3")
-        el += time.perf_counter() - t
-        reps += 1
+
+    def timed(variant, budget):
+        reps, el = 0, 0.0
+        while reps == 0 or el < budget:
+            t = time.perf_counter()
+            oracle.match(L, R, ocfg, nthreads=cores, variant=variant)
+            el += time.perf_counter() - t
+            reps += 1
+        return reps, el
+
+    reps, el = timed("v3", wall)
+    reps_s, el_s = timed("", wall)
+    shipped = reps_s * rows * W / el_s / 1e6
     return {
         "value": round(reps * rows * W / el / 1e6, 4),
         "unit": "Mpix/s",
         "cores": cores,
         "kind": "port",
-        "sample": "%d x %d of %d rows (x %d cols, n=%d) full match, %.1f s wall = %.0f CPU-s, "
-                  "oracle -O3 -march=x86-64-v3 -ffp-contract=off, %d threads"
+        "sample": "%d x %d of %d rows (x %d cols, n=%d), full match per row, %.1f s wall = %.0f "
+                  "CPU-s; per-frame rate extrapolated from the row sample (rows are "
+                  "independent); oracle -O3 -march=x86-64-v3 -ffp-contract=off, %d threads"
                   % (reps, rows, H, W, n, el, el * cores, cores),
+        "extrapolated_from_rows": rows,
         "ms_per_match_extrapolated": round(el / reps / rows * H * 1e3, 1),
+        "as_shipped_flags": {
+            "value": round(shipped, 4),
+            "ms_per_match_extrapolated": round(el_s / reps_s / rows * H * 1e3, 1),
+            "build": "oracle -O3 -ffp-contract=off, no -march (libgcc popcount, as the "
+                     "reference CMake build)",
+            "sample": "%d x %d rows, %.1f s wall" % (reps_s, rows, el_s),
+        },
+        "host": info,
     }
 
 

@@ -92,8 +92,10 @@ const char* bicos_last_error(void);
 /* --------------------------------------------------- device-resident API */
 
 /* Opaque per-device engine: owns a workspace (descriptor buffers, temporaries)
- * that grows on demand and is reused across calls. Not thread-safe per handle;
- * use one handle per host thread / stream. */
+ * that grows on demand (stream-ordered: hipFreeAsync / hipMallocAsync on the calling
+ * stream, never a device-wide synchronisation) and is reused across calls. Calls on one
+ * handle from several host threads are serialised by the engine's lock; the GPU work of
+ * calls on different streams is ordered through the engine's workspace event. */
 typedef struct bicos_engine bicos_engine;
 
 int bicos_engine_create(int device, bicos_engine** out);
@@ -161,7 +163,11 @@ int bicos_transform_device(const void* stack, int n, int rows, int cols, size_t 
                            size_t plane_pitch, int depth, int mode, int words, uint32_t* desc,
                            void* stream);
 /* flags: 1 = NODUPES, 2 = CONSISTENCY (reference impl/common.hpp:46-47). Consistency needs
- * the engine's workspace; out is int16 rows x cols (dense). */
+ * the engine's workspace; out is int16 rows x cols (dense).
+ * 256-bit descriptors (words = 8): bit 255 is ignored (masked on both sides). Every
+ * descriptor the transform produces leaves it zero -- LIMITED uses at most 4*65-6 = 254
+ * bits, FULL at most 16*16-2*16+3 = 227 -- so results on transform output are exact; a
+ * caller passing hand-made descriptors must keep bit 255 clear. */
 int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* desc1, int rows,
                         int cols, int words, int flags, int max_lr_diff, int16_t* out,
                         void* stream);

@@ -45,20 +45,24 @@ int check_hip(hipError_t e, const char* what) {
 
 const char* last_error() { return g_last_error.c_str(); }
 
-int reserve(void*& buf, size_t& have, size_t bytes, int device) {
+int reserve(void*& buf, size_t& have, size_t bytes, int device, hipStream_t st,
+            hipEvent_t ready) {
     if (bytes <= have && buf) return BICOS_OK;
     int cur = 0;
     (void)hipGetDevice(&cur);
     if (cur != device) (void)hipSetDevice(device);
+    int rc = BICOS_OK;
     if (buf) {
-        // in-flight work may still read the old buffer
-        (void)hipDeviceSynchronize();
-        (void)hipFree(buf);
+        // Stream-ordered: every earlier use of the old buffer, on any stream, is ordered
+        // before `ready` (recorded after each use), so `st` waits for it and frees the old
+        // buffer in its own order -- no device-wide synchronisation, nothing else stalls.
+        rc = check_hip(hipStreamWaitEvent(st, ready, 0), "hipStreamWaitEvent");
+        if (!rc) rc = check_hip(hipFreeAsync(buf, st), "hipFreeAsync(workspace)");
         buf = nullptr;
         have = 0;
     }
     const size_t want = bytes + bytes / 8;  // headroom for slightly larger calls
-    int rc = check_hip(hipMalloc(&buf, want), "hipMalloc(workspace)");
+    if (!rc) rc = check_hip(hipMallocAsync(&buf, want, st), "hipMallocAsync(workspace)");
     if (cur != device) (void)hipSetDevice(cur);
     if (rc != BICOS_OK) {
         buf = nullptr;
@@ -244,7 +248,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     const size_t keys = fused ? align_up((size_t)rows * glr.tiles_per_row * cols * 4) : 0;
     size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) +
                   (consistency ? (fused ? map16 + keys * (nodupes ? 2 : 1) : 2 * map16) : 0);
-    int rc = reserve(e->ws, e->ws_bytes, need, e->device);
+    int rc = reserve(e->ws, e->ws_bytes, need, e->device, st, e->ws_ready);
     if (rc) return rc;
     // order against earlier users of ws / stage on other streams; mark our use on exit
     rc = check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent");
@@ -470,7 +474,7 @@ int match_host(bicos_engine* e, const void* const* p0, const size_t* steps0,
     const size_t out_off = align_up((size_t)B * band_bytes);
     const size_t corr_off = out_off + align_up((size_t)rows * cols * dsz);
     const size_t total = corr_off + (corr ? (size_t)rows * cols * csz : 0);
-    int rc = reserve(e->stage, e->stage_bytes, total, e->device);
+    int rc = reserve(e->stage, e->stage_bytes, total, e->device, ks, e->ws_ready);
     if (rc) return rc;
     if (e->pinned_bytes < (size_t)K * band_bytes) {
         if (e->pinned) (void)hipHostFree(e->pinned);
@@ -672,8 +676,10 @@ void bicos_engine_destroy(bicos_engine* e) {
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(e->device);
     (void)hipDeviceSynchronize();
-    if (e->ws) (void)hipFree(e->ws);
-    if (e->stage) (void)hipFree(e->stage);
+    // workspaces come from the stream-ordered allocator (reserve)
+    if (e->ws) (void)hipFreeAsync(e->ws, e->own_stream);
+    if (e->stage) (void)hipFreeAsync(e->stage, e->own_stream);
+    (void)hipStreamSynchronize(e->own_stream);
     if (e->pinned) (void)hipHostFree(e->pinned);
     for (hipEvent_t ev : e->events) (void)hipEventDestroy(ev);
     e->pool.reset();
@@ -738,7 +744,11 @@ int bicos_match_device(bicos_engine* e, const void* stack0, const void* stack1, 
                        const BicosConfig* cfg, int has_nxcorr, void* disparity, void* corrmap,
                        void* stream) {
     if (!cfg) return fail(BICOS_E_ARG, "null config");
+    if (!e) return fail(BICOS_E_ARG, "null engine");
     try {
+        // the engine's workspace may be shared with other threads (the default engine is):
+        // enqueueing is serialised per engine, the GPU work is ordered through ws_ready
+        std::lock_guard<std::mutex> g(e->lock);
         // reference src/pybicos_c.cpp:59-61: a negative threshold keeps the default 0.5
         const float thr = cfg->nxcorr_threshold >= 0 ? cfg->nxcorr_threshold : 0.5f;
         return match_device(e, stack0, stack1, n, rows, cols, row_pitch, plane_pitch, depth, *cfg,
@@ -814,11 +824,13 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
         return check_hip(bicos_hip::launch_search(sa, g, words, nodupes, st), "search launch");
     }
     if (!e) return fail(BICOS_E_ARG, "consistency search needs an engine workspace");
+    std::lock_guard<std::mutex> lk(e->lock);  // the workspace may be shared (default engine)
     const size_t map16 = align_up((size_t)rows * cols * 2);
     if (!mx && fused_consistency()) {
         const bicos_hip::SearchGeometry glr = geometry_lr(e, rows, cols, words, nodupes);
         const size_t keys = align_up((size_t)rows * glr.tiles_per_row * cols * 4);
-        int rc = reserve(e->ws, e->ws_bytes, map16 + keys * (nodupes ? 2 : 1), e->device);
+        int rc = reserve(e->ws, e->ws_bytes, map16 + keys * (nodupes ? 2 : 1), e->device, st,
+                         e->ws_ready);
         if (rc) return rc;
         rc = check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent");
         if (rc) return rc;
@@ -840,7 +852,7 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
         (void)hipEventRecord(e->ws_ready, st);
         return rc;
     }
-    int rc = reserve(e->ws, e->ws_bytes, 2 * map16, e->device);
+    int rc = reserve(e->ws, e->ws_bytes, 2 * map16, e->device, st, e->ws_ready);
     if (rc) return rc;
     rc = check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent");
     if (rc) return rc;
@@ -1108,7 +1120,7 @@ void match(const std::vector<Image>& stack0, const std::vector<Image>& stack1, I
         row_pitch = rp0;
         plane_pitch = pp0;
     } else if (rows > 0 && cols > 0) {
-        throw_rc(reserve(e->stage, e->stage_bytes, 2 * n * plane_bytes, e->device));
+        throw_rc(reserve(e->stage, e->stage_bytes, 2 * n * plane_bytes, e->device, st, e->ws_ready));
         throw_rc(check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent"));
         char* dst = (char*)e->stage;
         const hipMemcpyKind kind = hipMemcpyDeviceToDevice;

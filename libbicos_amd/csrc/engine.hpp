@@ -79,8 +79,10 @@ void set_error(int code, const std::string& msg);
 int fail(int code, const std::string& msg);
 int check_hip(hipError_t e, const char* what);
 
-// Reserve `bytes` of engine workspace (device); returns BICOS_OK or an error code.
-int reserve(void*& buf, size_t& have, size_t bytes, int device);
+// Reserve `bytes` of engine workspace (device), stream-ordered on `st`: a buffer that
+// must grow is freed on `st` after `ready` (every earlier use) and the new one allocated
+// there (hipFreeAsync / hipMallocAsync). Returns BICOS_OK or an error code.
+int reserve(void*& buf, size_t& have, size_t bytes, int device, hipStream_t st, hipEvent_t ready);
 
 int descriptor_words(int n, int mode);
 

@@ -65,6 +65,20 @@ def _check_stack(t: torch.Tensor):
     return t.shape[0], t.shape[1], t.shape[2], t.stride(1), t.stride(0)
 
 
+def _check_out(t: torch.Tensor, name: str, shape, dtypes, device: torch.device) -> None:
+    """The kernels write rows*cols elements of the dtype the config implies straight through
+    the tensor's pointer: anything else would be an out-of-bounds HBM write."""
+    if t.device != device:
+        raise ValueError("%s must be on %s, got %s" % (name, device, t.device))
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError("%s must have shape %s, got %s" % (name, tuple(shape), tuple(t.shape)))
+    if t.dtype not in dtypes:
+        raise ValueError("%s must be %s for this config, got %s"
+                         % (name, " or ".join(str(d) for d in dtypes), t.dtype))
+    if not t.is_contiguous():
+        raise ValueError("%s must be contiguous (dense rows)" % name)
+
+
 def _stream(device: torch.device, stream=None) -> int:
     s = stream if stream is not None else torch.cuda.current_stream(device)
     return s.cuda_stream
@@ -124,14 +138,17 @@ class Engine:
             raise ValueError("stack1 must match stack0 in shape, strides and dtype")
         c, has_nxcorr = cfg.to_c()
         dev = stack0.device
+        disp_dtype = torch.float32 if has_nxcorr else torch.int16
+        corr_dtype = torch.float64 if cfg.precision else torch.float32
         if out is None:
-            out = torch.empty((rows, cols), dtype=torch.float32 if has_nxcorr else torch.int16,
-                              device=dev)
+            out = torch.empty((rows, cols), dtype=disp_dtype, device=dev)
+        _check_out(out, "out", (rows, cols), (disp_dtype,), dev)
         if has_nxcorr and want_corrmap and corrmap is None:
-            corrmap = torch.empty((rows, cols), device=dev,
-                                  dtype=torch.float64 if cfg.precision else torch.float32)
+            corrmap = torch.empty((rows, cols), device=dev, dtype=corr_dtype)
         if not (has_nxcorr and want_corrmap):
             corrmap = None
+        if corrmap is not None:
+            _check_out(corrmap, "corrmap", (rows, cols), (corr_dtype,), dev)
         rc = self._L.bicos_match_device(
             self._h, stack0.data_ptr(), stack1.data_ptr(), n, rows, cols, rp, pp, _depth(stack0),
             ctypes.byref(c), has_nxcorr, out.data_ptr(),
@@ -148,6 +165,7 @@ class Engine:
         pitch = self._L.bicos_desc_pitch(cols, words)
         if out is None:
             out = torch.empty((rows, pitch), dtype=torch.int32, device=stack.device)
+        _check_out(out, "out", (rows, pitch), (torch.int32,), stack.device)
         rc = self._L.bicos_transform_device(stack.data_ptr(), n, rows, cols, rp, pp,
                                             _depth(stack), mode, words, out.data_ptr(),
                                             _stream(stack.device, stream))
@@ -158,8 +176,15 @@ class Engine:
                flags: int = 1, max_lr_diff: int = -1, out: Optional[torch.Tensor] = None,
                stream=None) -> torch.Tensor:
         rows = desc0.shape[0]
+        pitch = self._L.bicos_desc_pitch(cols, words)
+        for name, d in (("desc0", desc0), ("desc1", desc1)):
+            if d.device != desc0.device or d.dtype != torch.int32 or not d.is_contiguous() or \
+                    d.dim() != 2 or tuple(d.shape) != (rows, pitch):
+                raise ValueError("%s must be a contiguous int32 [%d, %d] tensor on %s "
+                                 "(bicos_desc_pitch)" % (name, rows, pitch, desc0.device))
         if out is None:
             out = torch.empty((rows, cols), dtype=torch.int16, device=desc0.device)
+        _check_out(out, "out", (rows, cols), (torch.int16,), desc0.device)
         rc = self._L.bicos_search_device(self._h, desc0.data_ptr(), desc1.data_ptr(), rows, cols,
                                          words, flags, max_lr_diff, out.data_ptr(),
                                          _stream(desc0.device, stream))

@@ -1,0 +1,44 @@
+"""bench.py --gpus N without torchrun starts the N ranks itself (the way the driver runs the
+scaling bench); CPU only: the ranks rendezvous over gloo and rank 0 prints one JSON line."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra=None, timeout=240):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT,
+                          env=env, capture_output=True, text=True, timeout=timeout)
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_self_launch_starts_n_ranks(n):
+    p = _run(["--gpus", str(n), "--backend", "gloo", "--selftest-launch"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout  # rank 0 only
+    d = json.loads(lines[0])
+    assert d["world"] == n and d["gpus"] == n
+    assert d["rank_sum"] == n * (n + 1) / 2
+
+
+def test_single_gpu_runs_in_process():
+    p = _run(["--gpus", "1", "--selftest-launch"])
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["world"] == 1
+
+
+def test_failing_rank_fails_the_launch():
+    # rank 1 exits with status 3 before the rendezvous: the launcher stops rank 0 (which
+    # would wait for it forever) and reports the failure
+    p = _run(["--gpus", "2", "--backend", "gloo", "--selftest-launch"],
+             {"BICOS_SELFTEST_FAIL_RANK": "1"})
+    assert p.returncode == 3, (p.returncode, p.stderr[-2000:])

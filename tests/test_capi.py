@@ -115,3 +115,24 @@ def test_reference_python_wrapper_drives_our_abi(tmp_path, blib):
     assert c.precision == mod.Precision.SINGLE and c.nxcorr_threshold == 0.5
     assert np.isnan(mod.invalid_disparity(np.float32))
     assert mod.invalid_disparity(np.int16) == -32768
+
+
+def test_device_out_validation_rejects_bad_tensors():
+    """Engine.match / search / transform write through raw pointers: a wrong dtype, shape,
+    device or layout must raise before any launch (checked on CPU tensors, no GPU)."""
+    import torch
+    from libbicos_amd.device import _check_out
+    cpu = torch.device("cpu")
+    good = torch.empty((4, 6), dtype=torch.float32)
+    _check_out(good, "out", (4, 6), (torch.float32,), cpu)
+    with pytest.raises(ValueError, match="shape"):
+        _check_out(torch.empty((4, 5), dtype=torch.float32), "out", (4, 6), (torch.float32,), cpu)
+    with pytest.raises(ValueError, match="float64"):  # DOUBLE corrmap given a float32 tensor
+        _check_out(good, "corrmap", (4, 6), (torch.float64,), cpu)
+    with pytest.raises(ValueError, match="int16"):  # no-nxcorr disparity given float32
+        _check_out(good, "out", (4, 6), (torch.int16,), cpu)
+    with pytest.raises(ValueError, match="contiguous"):
+        _check_out(torch.empty((6, 4), dtype=torch.float32).t(), "out", (4, 6),
+                   (torch.float32,), cpu)
+    with pytest.raises(ValueError, match="must be on"):
+        _check_out(good, "out", (4, 6), (torch.float32,), torch.device("meta"))

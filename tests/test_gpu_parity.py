@@ -497,3 +497,96 @@ def test_mx_is_the_default_search(gpu):
     """The engine runs the matrix-core search unless tuned to a VALU variant."""
     from libbicos_amd import _lib
     assert "mx" in _lib.lib().bicos_build_info().decode()
+
+
+# ---------------------------------------------- cfg5: 4K frame, 8 row bands of 270
+def test_cfg5_full_size_and_bands(gpu, oracle):
+    """3840x2160x33 (BASELINE cfg5) on one GPU: oracle-checked rows of the whole-frame
+    match, and the 8 row bands of 270 the 8-GPU run computes are byte-identical to it."""
+    import torch
+    from libbicos_amd.device import MatchConfig
+    from libbicos_amd.distributed import band_rows
+    n, H, W = 33, 2160, 3840
+    cfg = dict(nxcorr_threshold=0.96)
+    L, R = stereo_stack(n, H, W)
+    s0, s1 = dev(L), dev(R)
+    full_d, full_c = gpu.match(s0, s1, MatchConfig(**cfg))
+    torch.cuda.synchronize()
+    got_d, got_c = host(full_d), host(full_c)
+    for (b, e) in [(0, 2), (1079, 1081), (2158, 2160)]:
+        rd, rc = oracle.match(L[:, b:e], R[:, b:e], oracle.OracleConfig(**cfg))
+        same(got_d[b:e].copy(), rd)
+        same(got_c[b:e].copy(), rc)
+    for r in range(8):
+        b, e = band_rows(H, 8, r)
+        assert e - b == 270
+        bd, bc = gpu.match(s0[:, b:e], s1[:, b:e], MatchConfig(**cfg))
+        same(host(bd), got_d[b:e])
+        same(host(bc), got_c[b:e])
+    truth = (16 + (48 * np.arange(H)) // H)[:, None]
+    d = got_d.astype(np.float64)
+    valid = np.isfinite(d) & (d != -32768)
+    assert valid.mean() > 0.95
+    assert (np.abs(d - truth)[valid] == 0).mean() > 0.99
+
+
+# ------------------------------------------------ the shared default engine, two threads
+def test_default_engine_two_threads(gpu, oracle):
+    """pybicos.match (host path) and device.match (device path) on the process-wide engine
+    from two threads at once: the engine lock + workspace event keep both exact."""
+    import threading
+    import torch
+    from libbicos_amd import device, pybicos
+    cfg = dict(nxcorr_threshold=0.9)
+    L1, R1 = stereo_stack(8, 96, 640, seed=11)
+    L2, R2 = stereo_stack(33, 64, 1300, seed=12)   # bigger: forces workspace growth
+    ref1 = oracle.match(L1, R1, oracle.OracleConfig(**cfg))
+    ref2 = oracle.match(L2, R2, oracle.OracleConfig(**cfg))
+    errors = []
+
+    def host_path():
+        try:
+            pc = pybicos.Config()
+            pc.nxcorr_threshold = 0.9
+            for _ in range(6):
+                d, c = pybicos.match(list(L1), list(R1), pc)
+                same(d, ref1[0])
+                same(c, ref1[1])
+        except Exception as ex:  # pragma: no cover - reported below
+            errors.append(ex)
+
+    def device_path():
+        try:
+            s0, s1 = dev(L2), dev(R2)
+            st = torch.cuda.Stream()
+            for _ in range(6):
+                with torch.cuda.stream(st):
+                    d, c = device.match(s0, s1, device.MatchConfig(**cfg))
+                st.synchronize()
+                same(host(d), ref2[0])
+                same(host(c), ref2[1])
+        except Exception as ex:  # pragma: no cover
+            errors.append(ex)
+
+    ts = [threading.Thread(target=host_path), threading.Thread(target=device_path)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+    assert not errors, errors
+
+
+def test_device_outputs_are_validated(gpu):
+    import torch
+    from libbicos_amd.device import MatchConfig
+    L, R = stereo_stack(8, 16, 64)
+    s0, s1 = dev(L), dev(R)
+    bad_corr = torch.empty((16, 64), dtype=torch.float32, device="cuda")
+    with pytest.raises(ValueError):  # DOUBLE writes float64
+        gpu.match(s0, s1, MatchConfig(precision=1), corrmap=bad_corr)
+    with pytest.raises(ValueError):  # no nxcorr: int16 disparity
+        gpu.match(s0, s1, MatchConfig(nxcorr_threshold=None),
+                  out=torch.empty((16, 64), dtype=torch.float32, device="cuda"))
+    with pytest.raises(ValueError):
+        gpu.match(s0, s1, MatchConfig(), out=torch.empty((16, 63), dtype=torch.float32,
+                                                         device="cuda"))

@@ -114,6 +114,14 @@ for step in "$@"; do
         pmcw) run pmcw 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/pmcw -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-path --kernel-reps 2 ;;
         pmcs) run pmcs 600 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE -d gpurun_out/pmcs -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-path --kernel-reps 2 ;;
         pmcl) run pmcl 600 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_ANY SQ_INSTS_VALU_INT32 TCC_HIT_sum TCC_MISS_sum -d gpurun_out/pmcl -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-host-path --kernel-reps 2 ;;
+        selflaunch2) run selflaunch2 600 python bench.py --gpus 2 --backend gloo --steps 5 --warmup 1 --no-cpu-baseline --no-host-path ;;
+        benchcfgs)  # one bench line per BASELINE config at N=1 (cfg2 with the CPU baseline)
+            run bench_cfg2 600 python bench.py --config cfg2 --steps 20 --warmup 3
+            for c in cfg3 cfg4 cfg5 cfg1; do
+                run bench_$c 600 python bench.py --config $c --steps 20 --warmup 3 --no-host-path --cpu-seconds 8
+            done ;;
+        profcfg)  # rocprofv3 kernel stats of one config (SC=cfgN)
+            run prof_${SC:-cfg2} 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${SC:-cfg2} -o run --output-format csv -- python bench.py --config ${SC:-cfg2} --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
         *) echo "unknown step $step" ;;
     esac
 done
