@@ -164,6 +164,11 @@ int bicos_transform_device(const void* stack, int n, int rows, int cols, size_t 
                            void* stream);
 /* flags: 1 = NODUPES, 2 = CONSISTENCY (reference impl/common.hpp:46-47). Consistency needs
  * the engine's workspace; out is int16 rows x cols (dense).
+ * flags bits 16-24 (optional): B = (flags >> 16) & 0x1FF, the number of low descriptor bits
+ * that may be set (0 = all). The caller promises bits B..32*words-1 are zero in both
+ * descriptor sets (true of transform output with B >= the transform's bit count: LIMITED
+ * 4n-6, FULL n^2-2n+3); the matrix-core search then skips the 64-bit K-steps above B
+ * (256-bit descriptors with B <= 192: 3 steps instead of 4). Results are unchanged.
  * 256-bit descriptors (words = 8): bit 255 is ignored (masked on both sides). Every
  * descriptor the transform produces leaves it zero -- LIMITED uses at most 4*65-6 = 254
  * bits, FULL at most 16*16-2*16+3 = 227 -- so results on transform output are exact; a

@@ -123,13 +123,19 @@ bool use_mx(const bicos_engine* e) {
     return env != 1;
 }
 
-bicos_hip::MxGeometry mx_geometry(const bicos_engine* e, int rows, int cols, int words) {
+// Highest descriptor bit the transform writes + 1 (an upper bound: LIMITED writes 4n-6 bits
+// for n >= 4, FULL n^2-2n+3; descriptor_transform.hpp:31-123). The search multiplies only
+// the 64-bit K-steps that hold them.
+int used_bits(int n, int mode) { return mode ? n * n - 2 * n + 3 : 4 * n - 5; }
+
+bicos_hip::MxGeometry mx_geometry(const bicos_engine* e, int rows, int cols, int words,
+                                  int bits = 0) {
     const bool tuned = e && e->tune_variant >= 64;
     // tuned: split = LDS stage KiB (0 = 64)
     const int lds = tuned && e->tune_split > 0 ? e->tune_split * 1024 : 64 * 1024;
     return bicos_hip::search_mx_geometry(rows, cols, words, lds, tuned ? e->tune_R : 0,
                                          tuned ? e->tune_waves : 0, e ? e->cus : 256,
-                                         tuned ? e->tune_variant - 64 : 0);
+                                         tuned ? e->tune_variant - 64 : 0, bits);
 }
 
 // The NoDuplicates search with the NXC agree fused into its epilogue (sa.out_f32 set): the
@@ -306,7 +312,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
         return launch_search_agree(e, sa, words, st);
     }
     if (mx) {
-        const bicos_hip::MxGeometry gm = mx_geometry(e, rows, cols, words);
+        const bicos_hip::MxGeometry gm = mx_geometry(e, rows, cols, words, used_bits(n, mode));
         if (!consistency) {
             bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
             rc = check_hip(bicos_hip::launch_search_mx(sa, gm, words, true, st), "search launch");
@@ -813,12 +819,13 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     hipStream_t st = (hipStream_t)stream;
     const size_t dpitch = bicos_desc_pitch(cols, words);
     const bool nodupes = (flags & 1) != 0;
+    const int bits = (flags >> 16) & 0x1FF;  // 0 = all descriptor bits may be set
     const bool mx = use_mx(e);
     const bicos_hip::SearchGeometry g = mx ? bicos_hip::SearchGeometry{} : geometry(e, rows, cols, words);
     if (!(flags & 2)) {
         bicos_hip::SearchArgs sa{desc0, desc1, out, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
         if (mx)
-            return check_hip(bicos_hip::launch_search_mx(sa, mx_geometry(e, rows, cols, words),
+            return check_hip(bicos_hip::launch_search_mx(sa, mx_geometry(e, rows, cols, words, bits),
                                                          words, nodupes, st),
                              "search launch");
         return check_hip(bicos_hip::launch_search(sa, g, words, nodupes, st), "search launch");
@@ -866,7 +873,7 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     bicos_hip::SearchArgs fa{desc0, desc1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
     bicos_hip::SearchArgs ra{desc1, desc0, rev, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
     if (mx) {
-        const bicos_hip::MxGeometry gm = mx_geometry(e, rows, cols, words);
+        const bicos_hip::MxGeometry gm = mx_geometry(e, rows, cols, words, bits);
         rc = check_hip(bicos_hip::launch_search_mx(fa, gm, words, nodupes, st), "search launch");
         if (rc) return rc;
         rc = check_hip(bicos_hip::launch_search_mx(ra, gm, words, nodupes, st),

@@ -111,9 +111,13 @@ struct MxGeometry {
     int T;                  // 32-col0 tiles per wave (2, 4, 8)
     int tiles_per_row;      // workgroups per row
     int keys;               // 1: one product + xor keys (cols <= 16384), 2: two products
+    int ksteps;             // 64-bit K-steps multiplied (<= words / 2; 3 for 256-bit
+                            // descriptors with <= 192 used bits)
 };
+// bits: highest used descriptor bit + 1 when the bits above are known to be zero (0 =
+// all of them)
 MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int T = 0,
-                              int waves = 0, int cus = 256, int keys = 0);
+                              int waves = 0, int cus = 256, int keys = 0, int bits = 0);
 hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool nodupes,
                             hipStream_t st);
 hipError_t launch_agree(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);

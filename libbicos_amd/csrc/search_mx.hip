@@ -103,7 +103,12 @@ __device__ __forceinline__ uint32_t umax3(uint32_t a, uint32_t b, uint32_t c) {
 __device__ __forceinline__ uint32_t fbits(float f) { return __builtin_bit_cast(uint32_t, f); }
 __device__ __forceinline__ float bitsf(uint32_t u) { return __builtin_bit_cast(float, u); }
 
-// min over the 16 keys of a D tile (bits ^ flip) and m; depth-3 tree of v_min3_u32
+constexpr uint32_t KEY_NONE = 0x7F000000u;  // above every key
+
+// min over the 16 keys of a D tile (bits ^ flip) and m; depth-3 tree of v_min3_u32. (The
+// keys are positive floats, so v_min3_f32 would do too; measured: it issues at the same half
+// rate as v_min3_u32 on gfx950 -- profiles/valu_rates_r02.jsonl -- and the search ran the
+// same, cfg2 0.400 vs 0.400 ms, cfg4 0.87 vs 0.86 ms.)
 __device__ __forceinline__ uint32_t min16(const v16f& d, uint32_t m, uint32_t flip) {
     // (element copied first: __builtin_bit_cast of a vector-element lvalue reads element 0)
     auto k = [&](int r) { return fbits(d[r]) ^ flip; };
@@ -153,14 +158,18 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 // blocks still do it). The result is exact whatever the data: the order only changes speed.
 // Keys stay relative to the base B of the block being reduced (shifts by the signed
 // B - B_prev); C = 768 + (8160 + col1 % 32) * 2^-14 keeps both fields in [0, 16383].
-template <int WORDS, bool NODUPES, int T, int KEYS, int FUSE = 0>
+template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, int FUSE = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void search_mx_kernel(SearchArgs a) {
     constexpr bool XK = KEYS != 0;
     constexpr bool FREE = KEYS == 2;
     static_assert(!FREE || NODUPES, "KEYS 2 is the NoDuplicates search");
     constexpr int K0 = FREE ? XKF_K0 : XK_K0;
-    constexpr int KS = WORDS >= 2 ? WORDS / 2 : 1;  // 64-bit K-steps
+    // 64-bit K-steps: KSU <= WORDS / 2 -- the steps past the highest descriptor bit the
+    // transform writes are all zero on both sides and contribute nothing (n = 40 LIMITED:
+    // 154 of 256 bits -> 3 steps, not 4)
+    constexpr int KS = KSU;
+    static_assert(KS >= 1 && 2 * KS <= (WORDS >= 2 ? WORDS : 2), "K-steps exceed the descriptor");
     constexpr int WL = 2 * KS;                      // LDS word slots per col1 (W=1: 1 pad)
     extern __shared__ __attribute__((aligned(16))) v4i lds_mx[];  // [WL][chunk]
 
@@ -195,7 +204,7 @@ void search_mx_kernel(SearchArgs a) {
             const int w = 2 * s + h;
             uint32_t x = 0;
             if (c0 < cols && w < WORDS) x = row0[(size_t)c0 * WORDS + w];
-            if (WORDS == 8 && w == 7) x &= 0x7FFFFFFFu;  // bit 255 masked (see below)
+            if (WORDS == 8 && KS == 4 && w == 7) x &= 0x7FFFFFFFu;  // bit 255 masked (see below)
             const v4i e = expand_bits(x);
 #pragma unroll
             for (int q = 0; q < 4; ++q) bf[t][s][q] = (int)(0x22222222u | ((uint32_t)e[q] << 3));
@@ -206,7 +215,7 @@ void search_mx_kernel(SearchArgs a) {
     int b2[T];  // KEYS 2: the base m2[t] is relative to (wave-uniform)
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-        m1[t] = XK ? XK_INF : 0xFFFFFFFFu;
+        m1[t] = XK ? XK_INF : KEY_NONE;
         m2[t] = XK ? XK_INF : 0u;
         b2[t] = 0;
     }
@@ -239,7 +248,7 @@ void search_mx_kernel(SearchArgs a) {
 #endif
         if constexpr (FREE) {
             const uint32_t m1s = m1[t] - (uint32_t)(B - bp);
-            const uint32_t bm = min16(d[t], 0xFFFFFFFFu, 0u);   // this half's block minimum
+            const uint32_t bm = min16(d[t], KEY_NONE, 0u);      // this half's block minimum
 #if defined(BICOS_MX_DIAG) && BICOS_MX_DIAG == 4  // timing only: the last-minimum path never runs
             const bool reach = bm <= (m1s | XK_COL) && bm == 0u;
 #else
@@ -292,7 +301,7 @@ void search_mx_kernel(SearchArgs a) {
             for (int w = 0; w < WL; ++w) {
                 uint32_t x = 0;
                 if (c1 < cols && w < WORDS) x = row1[(size_t)c1 * WORDS + w];
-                if (WORDS == 8 && w == 7) x &= 0x7FFFFFFFu;
+                if (WORDS == 8 && KS == 4 && w == 7) x &= 0x7FFFFFFFu;
                 const v4i ex = expand_bits(x);
                 v4i v;
 #pragma unroll
@@ -443,17 +452,17 @@ void search_mx_kernel(SearchArgs a) {
     }
 }
 
-template <int WORDS, bool NODUPES, int T, int KEYS>
+template <int WORDS, int KSU, bool NODUPES, int T, int KEYS>
 hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
-    constexpr int WL = WORDS >= 2 ? WORDS : 2;
+    constexpr int WL = 2 * KSU;
     const size_t lds = (size_t)WL * a.chunk * 16;
     // fused agree only with the NoDuplicates search (the pipeline's)
     auto pick = [&]() {
         if constexpr (NODUPES) {
-            if (a.out_f32) return a.depth == 2 ? search_mx_kernel<WORDS, NODUPES, T, KEYS, 2>
-                                               : search_mx_kernel<WORDS, NODUPES, T, KEYS, 1>;
+            if (a.out_f32) return a.depth == 2 ? search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 2>
+                                               : search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 1>;
         }
-        return search_mx_kernel<WORDS, NODUPES, T, KEYS, 0>;
+        return search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 0>;
     };
     if (a.out_f32 && (!NODUPES || (a.depth != 1 && a.depth != 2))) return hipErrorInvalidValue;
     const auto kern = pick();
@@ -472,26 +481,26 @@ constexpr bool mx_tiles_fit(int words, bool nodupes, int keys, int t) {
     return t <= 4 || (words == 1 && (keys != 0 || !nodupes)) || (words == 2 && !nodupes);
 }
 
-template <int WORDS, bool NODUPES, int KEYS>
+template <int WORDS, int KSU, bool NODUPES, int KEYS>
 hipError_t launch_mx_k(const SearchArgs& a, const MxGeometry& g, hipStream_t st) {
     if (g.T == 8) {
         if constexpr (mx_tiles_fit(WORDS, NODUPES, KEYS, 8)) {
-            return launch_mx<WORDS, NODUPES, 8, KEYS>(a, g.waves, st);
+            return launch_mx<WORDS, KSU, NODUPES, 8, KEYS>(a, g.waves, st);
         } else {  // does not fit: 4 tiles per wave, twice the workgroups per row
             SearchArgs b = a;
             const long per_wg = 32L * g.waves * 4;
             b.tiles_per_row = (int)((a.cols + per_wg - 1) / per_wg);
-            return launch_mx<WORDS, NODUPES, 4, KEYS>(b, g.waves, st);
+            return launch_mx<WORDS, KSU, NODUPES, 4, KEYS>(b, g.waves, st);
         }
     }
     switch (g.T) {
-        case 2: return launch_mx<WORDS, NODUPES, 2, KEYS>(a, g.waves, st);
-        case 4: return launch_mx<WORDS, NODUPES, 4, KEYS>(a, g.waves, st);
+        case 2: return launch_mx<WORDS, KSU, NODUPES, 2, KEYS>(a, g.waves, st);
+        case 4: return launch_mx<WORDS, KSU, NODUPES, 4, KEYS>(a, g.waves, st);
     }
     return hipErrorInvalidValue;
 }
 
-template <int WORDS, bool NODUPES>
+template <int WORDS, int KSU, bool NODUPES>
 hipError_t launch_mx_t(const SearchArgs& a, const MxGeometry& g, hipStream_t st) {
     // one-product XK keys by default: with NoDuplicates in any block order up to 8160
     // columns (BICOS_MX_ORDER=natural: ascending), ascending up to 16384; the two-product
@@ -502,25 +511,30 @@ hipError_t launch_mx_t(const SearchArgs& a, const MxGeometry& g, hipStream_t st)
     }();
     if (g.keys == 1) {
         if constexpr (NODUPES) {
-            if (a.cols <= XKF_MAX_COLS && !natural) return launch_mx_k<WORDS, NODUPES, 2>(a, g, st);
+            if (a.cols <= XKF_MAX_COLS && !natural) return launch_mx_k<WORDS, KSU, NODUPES, 2>(a, g, st);
         }
-        if (a.cols <= 16384) return launch_mx_k<WORDS, NODUPES, 1>(a, g, st);
+        if (a.cols <= 16384) return launch_mx_k<WORDS, KSU, NODUPES, 1>(a, g, st);
     }
-    return launch_mx_k<WORDS, NODUPES, 0>(a, g, st);
+    return launch_mx_k<WORDS, KSU, NODUPES, 0>(a, g, st);
 }
 
-template <int WORDS>
+template <int WORDS, int KSU>
 hipError_t launch_mx_w(const SearchArgs& a, const MxGeometry& g, bool nodupes, hipStream_t st) {
-    return nodupes ? launch_mx_t<WORDS, true>(a, g, st) : launch_mx_t<WORDS, false>(a, g, st);
+    return nodupes ? launch_mx_t<WORDS, KSU, true>(a, g, st) : launch_mx_t<WORDS, KSU, false>(a, g, st);
 }
 
 }  // namespace
 
 MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int T, int waves,
-                              int cus, int keys) {
+                              int cus, int keys, int bits) {
     MxGeometry g;
     g.keys = keys == 2 ? 2 : 1;
-    const int wl = words >= 2 ? words : 2;
+    // 64-bit K-steps the products need: all of the descriptor unless the caller knows that
+    // the bits past `bits` are zero (transform output); only 256-bit descriptors have a
+    // step to drop (129..192 used bits)
+    g.ksteps = words >= 2 ? words / 2 : 1;
+    if (words == 8 && bits > 0 && bits <= 192) g.ksteps = 3;
+    const int wl = 2 * g.ksteps;
     // LDS chunk of expanded right descriptors (16 B per word per col1), multiple of 32
     int chunk = lds_bytes / (wl * 16);
     chunk &= ~31;
@@ -531,11 +545,12 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     if (T) {
         g.T = T;
     } else {
-        // 4 tiles per wave (2 for 256-bit descriptors, whose 4-tile B fragments spill: cfg4
-        // 1.47 -> 1.09 ms, cfg4f 1.53 -> 0.64 ms; 8 spill for most widths), 2 when the grid
-        // would not give every CU about two workgroups (narrow row bands)
+        // 4 tiles per wave (2 for 4-step 256-bit descriptors, whose 4-tile B fragments
+        // spill: cfg4 1.47 -> 1.09 ms, cfg4f 1.53 -> 0.64 ms; at 3 steps 4 tiles win: cfg4
+        // 0.92 -> 0.82 ms; 8 spill for most widths), 2 when the grid would not give every
+        // CU about two workgroups (narrow row bands)
         g.T = 2;
-        for (int t = words >= 8 ? 2 : 4; t >= 2; t /= 2) {
+        for (int t = g.ksteps >= 4 ? 2 : 4; t >= 2; t /= 2) {
             const long per_wg = 32L * g.waves * t;
             const long nwg = (long)rows * ((cols + per_wg - 1) / per_wg);
             if (nwg >= 2L * (cus > 0 ? cus : 256)) {
@@ -557,10 +572,12 @@ hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool n
     a.chunk = g.chunk;
     a.tiles_per_row = g.tiles_per_row;
     switch (words) {
-        case 1: return launch_mx_w<1>(a, g, nodupes, st);
-        case 2: return launch_mx_w<2>(a, g, nodupes, st);
-        case 4: return launch_mx_w<4>(a, g, nodupes, st);
-        case 8: return launch_mx_w<8>(a, g, nodupes, st);
+        case 1: return launch_mx_w<1, 1>(a, g, nodupes, st);
+        case 2: return launch_mx_w<2, 1>(a, g, nodupes, st);
+        case 4: return launch_mx_w<4, 2>(a, g, nodupes, st);
+        case 8:
+            if (g.ksteps == 3) return launch_mx_w<8, 3>(a, g, nodupes, st);
+            return launch_mx_w<8, 4>(a, g, nodupes, st);
     }
     return hipErrorInvalidValue;
 }

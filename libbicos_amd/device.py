@@ -174,7 +174,12 @@ class Engine:
 
     def search(self, desc0: torch.Tensor, desc1: torch.Tensor, cols: int, words: int,
                flags: int = 1, max_lr_diff: int = -1, out: Optional[torch.Tensor] = None,
-               stream=None) -> torch.Tensor:
+               stream=None, bits: int = 0) -> torch.Tensor:
+        """bits: how many low descriptor bits may be set (0 = all; see used_bits) -- the
+        matrix-core search skips the K-steps above them (bicos_c.h flags bits 16-24)."""
+        if not 0 <= bits <= 256:
+            raise ValueError("bits must be in [0, 256]")
+        flags = (flags & 0xFFFF) | (bits << 16)
         rows = desc0.shape[0]
         pitch = self._L.bicos_desc_pitch(cols, words)
         for name, d in (("desc0", desc0), ("desc1", desc1)):
@@ -229,6 +234,12 @@ class Engine:
             out.data_ptr(), corr.data_ptr(), _stream(stack0.device, stream))
         _lib.check(rc, "bicos_search_agree_device")
         return out, corr
+
+
+def used_bits(n: int, mode: int = 0) -> int:
+    """Upper bound of the descriptor bits the transform sets (LIMITED 4n-6 for n >= 4,
+    FULL n^2-2n+3; reference descriptor_transform.hpp:31-123)."""
+    return n * n - 2 * n + 3 if mode else 4 * n - 5
 
 
 def descriptor_words(n: int, mode: int = 0) -> int:

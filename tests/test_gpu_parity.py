@@ -493,6 +493,34 @@ def test_mx_search_edges(gpu, oracle, words, W):
         gpu.tune(0, 0, 0, 0)
 
 
+@pytest.mark.parametrize("B", [129, 154, 192])
+def test_mx_search_used_bits(gpu, oracle, B):
+    """256-bit descriptors whose bits >= B are zero (transform output of n = 33..49
+    LIMITED): with the used-bits hint the search multiplies 3 K-steps instead of 4 and
+    still matches the oracle, for every flag combination and tile count."""
+    H, W, words = 3, 700, 8
+    rng = np.random.default_rng(B)
+    a = rng.integers(0, 2 ** 32, size=(H, W, words), dtype=np.uint64).astype(np.uint32)
+    b = a[:, np.roll(np.arange(W), 7)] ^ (rng.random((H, W, words)) < 0.05).astype(np.uint32)
+    b[1] = b[1, :1]             # every col1 ties on row 1
+    for arr in (a, b):
+        for w in range(words):
+            lo = 32 * w
+            if lo >= B:
+                arr[..., w] = 0
+            elif lo + 32 > B:
+                arr[..., w] &= np.uint32((1 << (B - lo)) - 1)
+    try:
+        for flags, lr in ((1, -1), (0, -1), (3, 1), (2, 0)):
+            ref = oracle.search(a, b, flags, lr)
+            for s in [(0, 0, 0, 0), (64, 2, 8, 0), (64, 4, 8, 0), (65, 4, 8, 0), (66, 2, 4, 0)]:
+                gpu.tune(*s)
+                out = host(gpu.search(dev(_pack(a)), dev(_pack(b)), W, words, flags, lr, bits=B))
+                same(out, ref)
+    finally:
+        gpu.tune(0, 0, 0, 0)
+
+
 def test_mx_is_the_default_search(gpu):
     """The engine runs the matrix-core search unless tuned to a VALU variant."""
     from libbicos_amd import _lib

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rows", type=int, default=0, help="row band size (0 = full frame)")
     ap.add_argument("--variants", default="32:2:4,16:2:4,16:4:4,16:2:8,16:4:8,16:2:2,16:4:2")
+    ap.add_argument("--all-bits", action="store_true", help="no used-bits hint (all K-steps)")
     args = ap.parse_args()
     C = bench.CONFIGS[args.config]
     n, H, W = C["n"], C["H"], C["W"]
@@ -41,6 +42,7 @@ def main():
     d0, d1 = eng.transform(s0, cfg.mode, words), eng.transform(s1, cfg.mode, words)
     flags = (2 | (1 if cfg.no_dupes else 0)) if cfg.variant == 1 else 1
     ops = bench.search_ops(rows, W, words, C["cfg"])
+    bits = 0 if args.all_bits else device.used_bits(n, cfg.mode)
     variants = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",")]
     variants = [v + (0,) * (4 - len(v)) for v in variants]
     times = {v: [] for v in variants}
@@ -49,7 +51,7 @@ def main():
     for rnd in range(args.rounds):
         for v in variants:
             eng.tune(*v)
-            out = eng.search(d0, d1, W, words, flags, cfg.max_lr_diff)
+            out = eng.search(d0, d1, W, words, flags, cfg.max_lr_diff, bits=bits)
             if rnd == 0:
                 torch.cuda.synchronize()
                 if ref is None:
@@ -59,7 +61,7 @@ def main():
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record(st)
             for _ in range(args.reps):
-                eng.search(d0, d1, W, words, flags, cfg.max_lr_diff, out=out)
+                eng.search(d0, d1, W, words, flags, cfg.max_lr_diff, out=out, bits=bits)
             b.record(st)
             torch.cuda.synchronize()
             times[v].append(a.elapsed_time(b) / args.reps)

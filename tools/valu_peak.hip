@@ -51,6 +51,15 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
             if (OP == 27) asm volatile("v_or_b32_sdwa %0, %1, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_0 src1_sel:DWORD" : "+v"(v[c]) : "v"(w[c]));
             if (OP == 28) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
             if (OP == 29) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(*(uint64_t*)&v[c & ~1]) : "v"(*(uint64_t*)&w[c & ~1]));
+            if (OP == 30) asm volatile("v_min3_f32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
+            if (OP == 31) asm volatile("v_min_f32 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 32) asm volatile("v_max3_f32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
+            if (OP == 33) asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(v[c]), "+v"(w[c]));
+            if (OP == 34) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
+            if (OP == 35) asm volatile("v_min_i32 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 36) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
+            if (OP == 37) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
+            if (OP == 38) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
             if (OP == 16) {  // the search loop's 128-bit mix per pair: 4 xor, 4 bcnt, lshl_or, med3, min
                 uint32_t t0, t1, t2, t3, cst, key;
                 asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t0) : "v"(v[c]), "v"(w[c]));
@@ -96,7 +105,8 @@ double run(const char* name, uint32_t* out, int grid) {
     return tops;
 }
 
-int main() {
+int main(int argc, char** argv) {
+    const bool only_new = argc > 1;  // any argument: the ops added in round 2 only
     hipDeviceProp_t p;
     hipGetDeviceProperties(&p, 0);
     int clk = 0;
@@ -108,6 +118,19 @@ int main() {
     uint32_t* out;
     hipMalloc(&out, 1 << 20);
     const int grid = p.multiProcessorCount * 8 * 4;  // 8 waves/SIMD worth of 256-thr blocks x4
+    run<30>("v_min3_f32", out, grid);
+    run<31>("v_min_f32", out, grid);
+    run<32>("v_max3_f32", out, grid);
+    run<33>("v_permlane32_swap_b32 (per instr)", out, grid);
+    run<34>("v_and_or_b32", out, grid);
+    run<35>("v_min_i32", out, grid);
+    run<36>("v_bfi_b32", out, grid);
+    run<37>("v_med3_f32", out, grid);
+    run<38>("v_add3_u32", out, grid);
+    if (only_new) {
+        hipFree(out);
+        return 0;
+    }
     run<0>("v_xor_b32", out, grid);
     run<1>("v_bcnt_u32_b32", out, grid);
     run<2>("v_min_u32", out, grid);
