@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "../../include/bicos/match.hpp"
+#include "../../include/bicos/hip.hpp"
 
 namespace bicos_impl {
 
@@ -1041,6 +1042,12 @@ static void throw_rc(int rc) {
 // reference src/impl/cpu.cpp:100-159 (validation, dispatch) + src/lib.cpp:31-49
 void match(const std::vector<Image>& stack0, const std::vector<Image>& stack1, Image& disparity,
            Config cfg, Image* corrmap, hipStream_t stream) {
+    impl::hip::match(stack0, stack1, disparity, cfg, corrmap, stream);
+}
+
+// the backend seam (bicos/hip.hpp; reference include/cpu.hpp:27-33, include/cuda.hpp:27-34)
+void impl::hip::match(const std::vector<Image>& stack0, const std::vector<Image>& stack1,
+                      Image& disparity, Config cfg, Image* corrmap, hipStream_t stream) {
     const size_t n = stack0.size();
     if (n < 2) throw Exception("need at least two images");
     if (stack1.size() != n) throw Exception("stacks differ in length");
@@ -1120,7 +1127,10 @@ void match(const std::vector<Image>& stack0, const std::vector<Image>& stack1, I
         return pp >= (size_t)rows * rp;
     };
     size_t rp0 = 0, pp0 = 0, rp1 = 0, pp1 = 0;
-    const size_t plane_bytes = (size_t)rows * cols * elem;
+    // staged rows start 64-byte aligned: no two copies share a dword and the pitches suit
+    // the aligned (LDS-staged) agree kernel
+    const size_t stage_row = ((size_t)cols * elem + 63) & ~(size_t)63;
+    const size_t plane_bytes = (size_t)rows * stage_row;
     if (uniform(stack0, rp0, pp0) && uniform(stack1, rp1, pp1) && rp0 == rp1 && pp0 == pp1) {
         s0 = stack0[0].data();
         s1 = stack1[0].data();
@@ -1132,17 +1142,19 @@ void match(const std::vector<Image>& stack0, const std::vector<Image>& stack1, I
         char* dst = (char*)e->stage;
         const hipMemcpyKind kind = hipMemcpyDeviceToDevice;
         for (size_t t = 0; t < n; ++t) {
-            throw_rc(check_hip(hipMemcpy2DAsync(dst + t * plane_bytes, cols * elem,
+            throw_rc(check_hip(hipMemcpy2DAsync(dst + t * plane_bytes, stage_row,
                                                 stack0[t].data(), stack0[t].step(), cols * elem,
                                                 rows, kind, st),
                                "stack upload"));
-            throw_rc(check_hip(hipMemcpy2DAsync(dst + (n + t) * plane_bytes, cols * elem,
+            throw_rc(check_hip(hipMemcpy2DAsync(dst + (n + t) * plane_bytes, stage_row,
                                                 stack1[t].data(), stack1[t].step(), cols * elem,
                                                 rows, kind, st),
                                "stack upload"));
         }
         s0 = dst;
         s1 = dst + n * plane_bytes;
+        row_pitch = stage_row / elem;
+        plane_pitch = plane_bytes / elem;
     }
 
     disparity.create(rows, cols, dtype, Memory::Device);

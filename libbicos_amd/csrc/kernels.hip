@@ -1209,8 +1209,14 @@ __global__ __launch_bounds__(256) void agree_lds_kernel(AgreeArgs a) {
     const uint32_t pp = (uint32_t)a.plane_pitch;
     const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
     int d = live ? (int)a.raw[(size_t)row * a.raw_pitch + col] : INVALID_I16;
+    // the range covers whole dwords: with a padded pitch and cols % 4 != 0 the stack's last
+    // pixel shares a dword with up to 3 bytes past it, and a dword reaching past
+    // num_records reads as 0 -- the last row's last pixels of plane n-1 came in as 0
+    // (tests/test_gpu_parity.py::test_padded_pitch_odd_width). Those bytes lie in the same
+    // aligned dword as valid pixels (base 4-aligned), so reading them cannot fault.
+    const uint32_t range = a.stack_bytes > 0xFFFFFFFCu ? 0xFFFFFFFFu : (a.stack_bytes + 3u) & ~3u;
     const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<void*>(a.stack0), (short)0, (int)a.stack_bytes, 0x00020000);
+        const_cast<void*>(a.stack0), (short)0, (int)range, 0x00020000);
     // left tile loads: pass j, wave-uniform plane p = j * WPP + tid / DW, dword tid % DW
     const int p0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x / DW);
     const uint32_t lane_b = (uint32_t)col0 * sizeof(TIn) + 4u * (threadIdx.x % DW);

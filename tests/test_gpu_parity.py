@@ -618,3 +618,30 @@ def test_device_outputs_are_validated(gpu):
     with pytest.raises(ValueError):
         gpu.match(s0, s1, MatchConfig(), out=torch.empty((16, 63), dtype=torch.float32,
                                                          device="cuda"))
+
+
+# ------------------------------------- padded row pitch with an odd image width
+@pytest.mark.parametrize("W,P,dt", [(190, 192, np.uint8), (190, 256, np.uint8), (301, 320, np.uint8),
+                                    (515, 576, np.uint8), (190, 192, np.uint16), (77, 80, np.uint16)])
+def test_padded_pitch_odd_width(gpu, oracle, W, P, dt):
+    """Stacks whose rows are padded to an aligned pitch while cols % 4 != 0 (what a
+    pitched allocation or the C++ staging path produces): the last pixels of the frame share
+    a dword with bytes past the stack; every stage must still read them (the aligned agree
+    kernel once read the last row's last pixels of plane n-1 as 0)."""
+    import torch
+    from libbicos_amd.device import MatchConfig
+    n, H = 10, 21
+    L, R = stereo_stack(n, H, W, dt)
+    tdt = torch.uint8 if dt == np.uint8 else torch.int16
+    buf = torch.zeros((2 * n, H, P), dtype=tdt, device="cuda")
+    buf[:n, :, :W] = dev(L)
+    buf[n:, :, :W] = dev(R)
+    for cfg in (dict(nxcorr_threshold=0.5), dict(nxcorr_threshold=0.5, mode=1),
+                dict(nxcorr_threshold=0.5, min_variance=1.0, subpixel_step=0.2),
+                dict(nxcorr_threshold=0.5, variant=1, max_lr_diff=2, no_dupes=True),
+                dict(nxcorr_threshold=None)):
+        rd, rc = oracle.match(L, R, oracle.OracleConfig(**cfg))
+        d, c = gpu.match(buf[:n, :, :W], buf[n:, :, :W], MatchConfig(**cfg))
+        same(host(d), rd)
+        if rc is not None:
+            same(host(c), rc)
