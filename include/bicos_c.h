@@ -105,11 +105,10 @@ bicos_engine* bicos_engine_default(int device);
 void bicos_engine_destroy(bicos_engine* e);
 
 /* Search-kernel tuning for this engine (0 = automatic for each argument):
- *   variant        VALU search: 16 = packed 16-bit keys, 17 = the same with the inner step
- *                  as one inline-asm block, 32 = 32-bit keys
- *   col0_per_lane  left pixels held in registers per lane (16: 2|4; 32: 1|2|4)
+ *   variant        16 = the VALU search (packed 16-bit keys)
+ *   col0_per_lane  left pixels held in registers per lane (2|4)
  *   waves          waves per workgroup (1..8)
- *   split          waves that share one col0 group and split its col1 scan (1|2|4|8, variant 16)
+ *   split          waves that share one col0 group and split its col1 scan (1|2|4|8)
  * Matrix-core search (search_mx.hip, the default): variant 64 (automatic keys), 65 (one FP4
  * product per pair + xor keys; rows <= 16384), 66 (two products: first / last minimum);
  * col0_per_lane = 32-column tiles per wave (2|4|8; 8 falls back to 4 where the registers do

@@ -109,7 +109,7 @@ bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, in
 }
 
 // Search implementation: the matrix-core search (search_mx.hip) unless the engine is tuned
-// to a VALU variant (bicos_engine_tune variant 16/17/18/32) or BICOS_SEARCH=valu;
+// to the VALU search (bicos_engine_tune variant 16) or BICOS_SEARCH=valu;
 // BICOS_SEARCH=mx forces it. Results are identical either way.
 bool use_mx(const bicos_engine* e) {
     static const int env = [] {
@@ -711,18 +711,14 @@ int bicos_engine_tune(bicos_engine* e, int variant, int col0_per_lane, int waves
         e->tune_split = split;
         return BICOS_OK;
     }
-    if (variant != 0 && variant != 16 && variant != 17 && variant != 18 && variant != 32)
-        return fail(BICOS_E_ARG, "variant 0|16|17|18|32|64|65|66");
-    const int v = (variant == 17 || variant == 18) ? 16 : (variant ? variant : 16);
-    if (col0_per_lane != 0 && !(v == 16 ? (col0_per_lane == 2 || col0_per_lane == 4)
-                                        : (col0_per_lane == 1 || col0_per_lane == 2 ||
-                                           col0_per_lane == 4)))
-        return fail(BICOS_E_ARG, "col0_per_lane: 2|4 (variant 16), 1|2|4 (variant 32)");
+    if (variant != 0 && variant != 16) return fail(BICOS_E_ARG, "variant 0|16|64|65|66");
+    if (col0_per_lane != 0 && col0_per_lane != 2 && col0_per_lane != 4)
+        return fail(BICOS_E_ARG, "col0_per_lane: 2|4 (variant 16)");
     if (waves < 0 || waves > 8) return fail(BICOS_E_ARG, "waves 1..8");
     if (split != 0 && split != 1 && split != 2 && split != 4 && split != 8)
         return fail(BICOS_E_ARG, "split 1|2|4|8");
-    if (split > 1 && (v != 16 || (waves ? waves : 8) % split))
-        return fail(BICOS_E_ARG, "split needs variant 16 and waves divisible by split");
+    if (split > 1 && (waves ? waves : 8) % split)
+        return fail(BICOS_E_ARG, "split needs waves divisible by split");
     e->tune_variant = variant;
     e->tune_R = col0_per_lane;
     e->tune_waves = waves;

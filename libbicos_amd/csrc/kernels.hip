@@ -1,7 +1,9 @@
 // kernels.hip -- gfx950 (CDNA4) kernels of the BICOS hot path.
 //
 //   transform_kernel    descriptor_transform  (reference include/impl/cpu/descriptor_transform.hpp:31-138)
-//   search_kernel       bicos Hamming search  (reference include/impl/cpu/bicos.hpp:29-113)
+//   search16_kernel     bicos Hamming search on the VALU (reference include/impl/cpu/bicos.hpp:29-113;
+//                       the default search runs on the matrix cores: search_mx.hip)
+//   search_lr_kernel    the same, Consistency's forward + reverse minima in one pass
 //   consistency_kernel  left-right check      (reference include/impl/cpu/bicos.hpp:99-106)
 //   agree_kernel        NXC filter            (reference include/impl/cpu/agree.hpp:28-93)
 //   subpixel_kernel     NXC + quadratic refine(reference include/impl/cpu/agree.hpp:95-191)
@@ -43,10 +45,6 @@ __device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t acc) {
     return __builtin_popcount(x) + acc;
 }
 
-// median of three -> v_med3_u32 (pattern-matched by the backend)
-__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
-    return max(min(a, b), min(max(a, b), c));
-}
 
 using nxc::ld;
 using nxc::fma_p;
@@ -378,117 +376,14 @@ __device__ __forceinline__ void lds_fetch(const uint32_t* s, uint32_t (&d)[WORDS
     }
 }
 
-template <int WORDS, bool NODUPES, int R>
-__device__ __forceinline__ void search_step(const uint32_t* s, uint32_t c1,
-                                            const uint32_t (&d0)[R][WORDS], uint32_t (&best)[R],
-                                            uint32_t (&second)[R]) {
-    uint32_t d1[WORDS];
-    lds_fetch<WORDS>(s, d1);
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const uint32_t key = (ham<WORDS>(d0[r], d1) << 16) | c1;
-        if (NODUPES) second[r] = umed3(best[r], key, second[r]);
-        best[r] = min(best[r], key);
-    }
-}
-
-// One workgroup = one (row, col0 tile). The tile's WAVES*64*R left descriptors live in
-// registers (R per lane, lanes on consecutive columns); the right row is staged through
-// LDS in chunks of `chunk` columns and read back as wave-uniform broadcasts. For every
-// col1 each lane updates, per held col0,
-//     key    = cost << 16 | col1                     (v_lshl_or_b32, col1 in an SGPR)
-//     second = med3(best, key, second)              (v_med3_u32)
-//     best   = min(best, key)                       (v_min_u32)
-// so `best` is the argmin with the lowest col1 among equal costs (the reference's strict
-// '<' scan) and the minimum is duplicated iff cost(second) == cost(best).
-//   out_mode 0: out = col0 - best_col1 (INVALID_I16 when rejected)      [disparity]
-//   out_mode 1: out = best_col1 (-1 when rejected)                      [Consistency passes]
-template <int WORDS, bool NODUPES, int R>
-__global__ __launch_bounds__(512) void search_kernel(SearchArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-
-    // XCD-aware tile order: hardware deals workgroups round-robin over the 8 XCDs; give
-    // each XCD a contiguous range of (row, tile) so the tiles of one row share one L2.
-    const int nwg = gridDim.x;
-    const int bid = blockIdx.x;
-    const int per_xcd = (nwg + 7) / 8;
-    int logical = (bid % 8) * per_xcd + bid / 8;
-    // grids whose size is not a multiple of 8 leave holes at the end of the last XCDs'
-    // ranges; fold them back onto the identity map so the mapping stays a bijection
-    if (nwg % 8 != 0) logical = bid;
-    const int row = logical / a.tiles_per_row;
-    const int tile = logical % a.tiles_per_row;
-
-    const int waves = blockDim.x / 64;
-    const int wave = threadIdx.x / 64;
-    const int lane = threadIdx.x % 64;
-    const int cols = a.cols;
-    const int col0_base = tile * waves * 64 * R + wave * 64 * R + lane;
-
-    const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
-    const uint32_t* __restrict__ row1 = a.desc1 + (size_t)row * a.desc_pitch;
-
-    uint32_t d0[R][WORDS];
-    uint32_t best[R], second[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int c0 = col0_base + r * 64;
-        const int cc = c0 < cols ? c0 : cols - 1;
-        lds_fetch<WORDS>(row0 + (size_t)cc * WORDS, d0[r]);
-        best[r] = 0xFFFFFFFFu;
-        second[r] = 0xFFFFFFFFu;
-    }
-
-    for (int base = 0; base < cols; base += a.chunk) {
-        const int ncols = min(a.chunk, cols - base);
-        const int nwords = ncols * WORDS;
-        if (base) __syncthreads();
-        {
-            const uint32_t* src = row1 + (size_t)base * WORDS;
-            const int n4 = nwords / 4;
-            for (int i = threadIdx.x; i < n4; i += blockDim.x)
-                ((uint4*)lds)[i] = ((const uint4*)src)[i];
-            for (int i = n4 * 4 + threadIdx.x; i < nwords; i += blockDim.x) lds[i] = src[i];
-        }
-        __syncthreads();
-
-        // Static-count inner unroll: the bcnt asm is convergent, which forbids the
-        // compiler's runtime unrolling; U LDS broadcasts are issued ahead of the VALU.
-        constexpr int U = WORDS >= 8 ? 4 : 8;
-        int j = 0;
-        for (; j + U <= ncols; j += U) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) search_step<WORDS, NODUPES, R>(lds + (j + u) * WORDS,
-                                                                     (uint32_t)(base + j + u), d0,
-                                                                     best, second);
-        }
-        for (; j < ncols; ++j)
-            search_step<WORDS, NODUPES, R>(lds + j * WORDS, (uint32_t)(base + j), d0, best, second);
-    }
-
-    int16_t* __restrict__ out = a.out + (size_t)row * a.out_pitch;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int c0 = col0_base + r * 64;
-        if (c0 >= cols) continue;
-        const int b = (int)(best[r] & 0xFFFFu);
-        const bool dup = NODUPES && ((second[r] >> 16) == (best[r] >> 16));
-        int16_t v;
-        if (a.out_mode == 0)
-            v = dup ? INVALID_I16 : (int16_t)(c0 - b);
-        else
-            v = dup ? (int16_t)-1 : (int16_t)b;
-        out[c0] = v;
-    }
-}
-
-// ---- packed 16-bit key variant ---------------------------------------------------
+// ---- the VALU search: packed 16-bit keys ------------------------------------------
 //
 // Measured on MI355X (tools/valu_peak.hip): v_xor/v_and/v_add issue at full rate
 // (~72 T lane-op/s) but v_bcnt, v_min, v_med3, v_lshl_or, v_perm and v_pk_*_u16 at half
-// rate (~38.5 T). The 32-bit-key loop above spends 7 half-rate ops per pair (w bcnt +
-// lshl_or + med3 + min for w = 4). Here two col0 share one 32-bit register of two 16-bit
-// keys (cost << 8 | col1 within a 256-column tile):
+// rate (~38.5 T). A direct 32-bit-key loop (cost << 16 | col1 per pair, v_med3 + v_min)
+// spends 7 half-rate ops per pair for w = 4 (measured 11 % slower; removed in round 2, as
+// were two hand-scheduled forms of this loop). Here two col0 share one 32-bit register
+// of two 16-bit keys (cost << 8 | col1 within a 256-column tile):
 //   r0, r1  = bcnt chains seeded with (col1_local << 8)  -> byte1 = col1, byte0 = cost
 //   key     = v_perm_b32(r1, r0)      [r0.b1 r0.b0 | r1.b1 r1.b0]  (1 op / 2 pairs)
 //   lo      = v_pk_min_u16(lo, key)   first minimum (lowest col1)  (1 op / 2 pairs)
@@ -504,88 +399,6 @@ __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
                                                                   __builtin_bit_cast(u16x2, b)));
 }
 
-// One col1 step for one packed pair (col0 a -> low half, col0 b -> high half) as ONE asm
-// block: hipcc pads every use of a value defined by an asm statement with an s_nop, and
-// lets the compiler re-associate the bcnt chain into v_add3 trees otherwise; measured
-// (tools/search_variants.hip): full-asm step 1.6-8 % faster than the asm-opaque chain,
-// 25 % faster than plain C. Emitted per word k: two v_xor (full rate) + two v_bcnt chained
-// through r0/r1 (seeded with col1_local << 8 by the first bcnt); then one v_perm_b32 and
-// v_pk_min_u16 for the first minimum, one v_xor + v_pk_min_u16 for the last minimum.
-#define BICOS_XB(k, first)                                      \
-    "v_xor_b32 %[t0], %[d" #k "], %[a" #k "]\n\t"                \
-    "v_xor_b32 %[t1], %[d" #k "], %[b" #k "]\n\t"                \
-    "v_bcnt_u32_b32 %[r0], %[t0], " first "\n\t"                \
-    "v_bcnt_u32_b32 %[r1], %[t1], " first "\n\t"
-#define BICOS_XB_NEXT(k)                                        \
-    "v_xor_b32 %[t0], %[d" #k "], %[a" #k "]\n\t"                \
-    "v_xor_b32 %[t1], %[d" #k "], %[b" #k "]\n\t"                \
-    "v_bcnt_u32_b32 %[r0], %[t0], %[r0]\n\t"                    \
-    "v_bcnt_u32_b32 %[r1], %[t1], %[r1]\n\t"
-#define BICOS_PACK_MIN                                          \
-    "v_perm_b32 %[r0], %[r1], %[r0], %[sel]\n\t"                \
-    "v_pk_min_u16 %[lo], %[lo], %[r0]\n\t"
-#define BICOS_PACK_MAX_TOO                                      \
-    "v_xor_b32 %[r0], 0xff00ff, %[r0]\n\t"                      \
-    "v_pk_min_u16 %[hi], %[hi], %[r0]\n\t"
-#define BICOS_OPS4(o)                                                                    \
-    [d0] "v"(d1[o + 0]), [d1] "v"(d1[o + 1]), [d2] "v"(d1[o + 2]), [d3] "v"(d1[o + 3]),  \
-        [a0] "v"(a[o + 0]), [a1] "v"(a[o + 1]), [a2] "v"(a[o + 2]), [a3] "v"(a[o + 3]),  \
-        [b0] "v"(b[o + 0]), [b1] "v"(b[o + 1]), [b2] "v"(b[o + 2]), [b3] "v"(b[o + 3])
-
-template <int WORDS, bool HI>
-__device__ __forceinline__ void pair_step(const uint32_t (&d1)[WORDS], const uint32_t (&a)[WORDS],
-                                          const uint32_t (&b)[WORDS], uint32_t seed, uint32_t& lo,
-                                          uint32_t& hi) {
-    uint32_t t0, t1, r0, r1;
-    const uint32_t sel = 0x04050001u;  // key = [r0.b1 r0.b0 | r1.b1 r1.b0]
-    if constexpr (WORDS == 1) {
-        if (HI)
-            asm(BICOS_XB(0, "%[seed]") BICOS_PACK_MIN BICOS_PACK_MAX_TOO
-                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1), [lo] "+v"(lo), [hi] "+v"(hi)
-                : [d0] "v"(d1[0]), [a0] "v"(a[0]), [b0] "v"(b[0]), [seed] "s"(seed), [sel] "s"(sel));
-        else
-            asm(BICOS_XB(0, "%[seed]") BICOS_PACK_MIN
-                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1), [lo] "+v"(lo)
-                : [d0] "v"(d1[0]), [a0] "v"(a[0]), [b0] "v"(b[0]), [seed] "s"(seed), [sel] "s"(sel));
-    } else if constexpr (WORDS == 2) {
-        if (HI)
-            asm(BICOS_XB(0, "%[seed]") BICOS_XB_NEXT(1) BICOS_PACK_MIN BICOS_PACK_MAX_TOO
-                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1), [lo] "+v"(lo), [hi] "+v"(hi)
-                : [d0] "v"(d1[0]), [d1] "v"(d1[1]), [a0] "v"(a[0]), [a1] "v"(a[1]), [b0] "v"(b[0]),
-                  [b1] "v"(b[1]), [seed] "s"(seed), [sel] "s"(sel));
-        else
-            asm(BICOS_XB(0, "%[seed]") BICOS_XB_NEXT(1) BICOS_PACK_MIN
-                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1), [lo] "+v"(lo)
-                : [d0] "v"(d1[0]), [d1] "v"(d1[1]), [a0] "v"(a[0]), [a1] "v"(a[1]), [b0] "v"(b[0]),
-                  [b1] "v"(b[1]), [seed] "s"(seed), [sel] "s"(sel));
-    } else if constexpr (WORDS == 4) {
-        if (HI)
-            asm(BICOS_XB(0, "%[seed]") BICOS_XB_NEXT(1) BICOS_XB_NEXT(2) BICOS_XB_NEXT(3)
-                    BICOS_PACK_MIN BICOS_PACK_MAX_TOO
-                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1), [lo] "+v"(lo), [hi] "+v"(hi)
-                : BICOS_OPS4(0), [seed] "s"(seed), [sel] "s"(sel));
-        else
-            asm(BICOS_XB(0, "%[seed]") BICOS_XB_NEXT(1) BICOS_XB_NEXT(2) BICOS_XB_NEXT(3)
-                    BICOS_PACK_MIN
-                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1), [lo] "+v"(lo)
-                : BICOS_OPS4(0), [seed] "s"(seed), [sel] "s"(sel));
-    } else {
-        // 8 words: two blocks (inline asm takes at most 30 operands)
-        asm(BICOS_XB(0, "%[seed]") BICOS_XB_NEXT(1) BICOS_XB_NEXT(2) BICOS_XB_NEXT(3)
-            : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "=&v"(r0), [r1] "=&v"(r1)
-            : BICOS_OPS4(0), [seed] "s"(seed));
-        if (HI)
-            asm(BICOS_XB_NEXT(0) BICOS_XB_NEXT(1) BICOS_XB_NEXT(2) BICOS_XB_NEXT(3)
-                    BICOS_PACK_MIN BICOS_PACK_MAX_TOO
-                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "+&v"(r0), [r1] "+&v"(r1), [lo] "+v"(lo), [hi] "+v"(hi)
-                : BICOS_OPS4(4), [sel] "s"(sel));
-        else
-            asm(BICOS_XB_NEXT(0) BICOS_XB_NEXT(1) BICOS_XB_NEXT(2) BICOS_XB_NEXT(3) BICOS_PACK_MIN
-                : [t0] "=&v"(t0), [t1] "=&v"(t1), [r0] "+&v"(r0), [r1] "+&v"(r1), [lo] "+v"(lo)
-                : BICOS_OPS4(4), [sel] "s"(sel));
-    }
-}
-
 // The same step in C with an instruction-free asm keeping each bcnt accumulator opaque
 // (so the chain is not re-associated into v_add3); the compiler schedules freely.
 template <int WORDS>
@@ -597,26 +410,7 @@ __device__ __forceinline__ uint32_t ham_seeded(const uint32_t (&a)[WORDS], const
     return c;
 }
 
-// Both col0 chains interleaved word by word; one instruction-free asm per word keeps the
-// two accumulators opaque (no v_add3 re-association) and the first v_bcnt takes the
-// col1 seed straight from its SGPR.
-template <int WORDS>
-__device__ __forceinline__ void ham_pair(const uint32_t (&a)[WORDS], const uint32_t (&b)[WORDS],
-                                         const uint32_t (&d)[WORDS], uint32_t seed, uint32_t& r0,
-                                         uint32_t& r1) {
-    uint32_t c0 = __builtin_popcount(a[0] ^ d[0]) + seed;
-    uint32_t c1 = __builtin_popcount(b[0] ^ d[0]) + seed;
-#pragma unroll
-    for (int k = 1; k < WORDS; ++k) {
-        asm("" : "+v"(c0), "+v"(c1));
-        c0 = __builtin_popcount(a[k] ^ d[k]) + c0;
-        c1 = __builtin_popcount(b[k] ^ d[k]) + c1;
-    }
-    r0 = c0;
-    r1 = c1;
-}
-
-template <int WORDS, bool NODUPES, int RP, int STEP>
+template <int WORDS, bool NODUPES, int RP>
 __device__ __forceinline__ void search16_step(const uint32_t* s, uint32_t seed,
                                               const uint32_t (&d0)[2 * RP][WORDS],
                                               uint32_t (&lo)[RP], uint32_t (&hi)[RP]) {
@@ -624,27 +418,17 @@ __device__ __forceinline__ void search16_step(const uint32_t* s, uint32_t seed,
     lds_fetch<WORDS>(s, d1);
 #pragma unroll
     for (int p = 0; p < RP; ++p) {
-        if (STEP == 1) {
-            pair_step<WORDS, NODUPES>(d1, d0[2 * p], d0[2 * p + 1], seed, lo[p], hi[p]);
-        } else if (STEP == 2) {
-            uint32_t r0, r1;
-            ham_pair<WORDS>(d0[2 * p], d0[2 * p + 1], d1, seed, r0, r1);
-            const uint32_t key = __builtin_amdgcn_perm(r1, r0, 0x04050001u);
-            lo[p] = pk_min_u16(lo[p], key);
-            if (NODUPES) hi[p] = pk_min_u16(hi[p], key ^ 0x00FF00FFu);
-        } else {
-            const uint32_t r0 = ham_seeded<WORDS>(d0[2 * p], d1, seed);
-            const uint32_t r1 = ham_seeded<WORDS>(d0[2 * p + 1], d1, seed);
-            const uint32_t key = __builtin_amdgcn_perm(r1, r0, 0x04050001u);
-            lo[p] = pk_min_u16(lo[p], key);
-            if (NODUPES) hi[p] = pk_min_u16(hi[p], key ^ 0x00FF00FFu);
-        }
+        const uint32_t r0 = ham_seeded<WORDS>(d0[2 * p], d1, seed);
+        const uint32_t r1 = ham_seeded<WORDS>(d0[2 * p + 1], d1, seed);
+        const uint32_t key = __builtin_amdgcn_perm(r1, r0, 0x04050001u);
+        lo[p] = pk_min_u16(lo[p], key);
+        if (NODUPES) hi[p] = pk_min_u16(hi[p], key ^ 0x00FF00FFu);
     }
 }
 
 // FUSE: 0 = plain search (int16 `out`), 1 / 2 = fused NXC agree epilogue on u8 / u16
 // stacks (agree.hpp:53-93 for the pixels this workgroup owns; see SearchArgs)
-template <int WORDS, bool NODUPES, int RP, int STEP, int FUSE = 0>
+template <int WORDS, bool NODUPES, int RP, int FUSE = 0>
 __global__ __launch_bounds__(512) void search16_kernel(SearchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
 
@@ -717,11 +501,11 @@ __global__ __launch_bounds__(512) void search16_kernel(SearchArgs a) {
             for (; j + U <= tn; j += U) {
 #pragma unroll
                 for (int u = 0; u < U; ++u)
-                    search16_step<WORDS, NODUPES, RP, STEP>(tl + (j + u) * WORDS,
+                    search16_step<WORDS, NODUPES, RP>(tl + (j + u) * WORDS,
                                                             (uint32_t)(j + u) << 8, d0, lo, hi);
             }
             for (; j < tn; ++j)
-                search16_step<WORDS, NODUPES, RP, STEP>(tl + j * WORDS, (uint32_t)j << 8, d0, lo,
+                search16_step<WORDS, NODUPES, RP>(tl + j * WORDS, (uint32_t)j << 8, d0, lo,
                                                         hi);
 
             // fold the tile's 16-bit keys into 32-bit (cost << 16 | col1) keys
@@ -1508,64 +1292,33 @@ hipError_t launch_transform_t(const TransformArgs& a, int mode, int words, hipSt
     return hipErrorInvalidValue;
 }
 
-template <int WORDS, bool NODUPES, int R>
-hipError_t launch_search_r(const SearchArgs& a, int waves, hipStream_t st) {
-    const size_t lds = (size_t)a.chunk * WORDS * 4;
-    const int nwg = a.rows * a.tiles_per_row;
-    hipLaunchKernelGGL((search_kernel<WORDS, NODUPES, R>), dim3(nwg), dim3(64 * waves), lds, st, a);
-    return hipGetLastError();
-}
-
-template <int WORDS, bool NODUPES, int RP, int STEP>
+template <int WORDS, bool NODUPES, int RP>
 hipError_t launch_search16_r(const SearchArgs& a, int waves, hipStream_t st) {
     const size_t stage = (size_t)a.chunk * WORDS * 4;
     const size_t merge = a.split > 1 ? (size_t)(waves / a.split) * 64 * (2 * RP) * 8 * (a.split - 1) : 0;
     const size_t lds = stage > merge ? stage : merge;
     const int nwg = a.rows * a.tiles_per_row;
-    if constexpr (NODUPES && STEP == 0) {
+    if constexpr (NODUPES) {
         if (a.out_f32) {
             if (a.depth == 1)
-                hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP, STEP, 1>), dim3(nwg),
+                hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP, 1>), dim3(nwg),
                                    dim3(64 * waves), lds, st, a);
             else
-                hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP, STEP, 2>), dim3(nwg),
+                hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP, 2>), dim3(nwg),
                                    dim3(64 * waves), lds, st, a);
             return hipGetLastError();
         }
     }
-    if (a.out_f32) return hipErrorInvalidValue;  // fused agree: NoDuplicates, variant 16 only
-    hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP, STEP>), dim3(nwg), dim3(64 * waves), lds,
-                       st, a);
+    if (a.out_f32) return hipErrorInvalidValue;  // fused agree: NoDuplicates only
+    hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP>), dim3(nwg), dim3(64 * waves), lds, st, a);
     return hipGetLastError();
 }
 
 template <int WORDS, bool NODUPES>
 hipError_t launch_search_n(const SearchArgs& a, const SearchGeometry& g, hipStream_t st) {
-    if (g.variant == 16) {
-        switch (g.R) {
-            case 2: return launch_search16_r<WORDS, NODUPES, 1, 0>(a, g.waves, st);
-            case 4: return launch_search16_r<WORDS, NODUPES, 2, 0>(a, g.waves, st);
-        }
-        return hipErrorInvalidValue;
-    }
-    if (g.variant == 17) {
-        switch (g.R) {
-            case 2: return launch_search16_r<WORDS, NODUPES, 1, 1>(a, g.waves, st);
-            case 4: return launch_search16_r<WORDS, NODUPES, 2, 1>(a, g.waves, st);
-        }
-        return hipErrorInvalidValue;
-    }
-    if (g.variant == 18) {
-        switch (g.R) {
-            case 2: return launch_search16_r<WORDS, NODUPES, 1, 2>(a, g.waves, st);
-            case 4: return launch_search16_r<WORDS, NODUPES, 2, 2>(a, g.waves, st);
-        }
-        return hipErrorInvalidValue;
-    }
     switch (g.R) {
-        case 1: return launch_search_r<WORDS, NODUPES, 1>(a, g.waves, st);
-        case 2: return launch_search_r<WORDS, NODUPES, 2>(a, g.waves, st);
-        case 4: return launch_search_r<WORDS, NODUPES, 4>(a, g.waves, st);
+        case 2: return launch_search16_r<WORDS, NODUPES, 1>(a, g.waves, st);
+        case 4: return launch_search16_r<WORDS, NODUPES, 2>(a, g.waves, st);
     }
     return hipErrorInvalidValue;
 }
@@ -1657,7 +1410,8 @@ hipError_t launch_transform(TransformArgs a, int depth, int mode, int words, hip
 SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes, int variant,
                                int R, int waves, int split, int cus, int extra_col_bytes) {
     SearchGeometry g;
-    g.variant = (variant == 32 || variant == 17 || variant == 18) ? variant : 16;
+    (void)variant;  // one VALU search remains: packed 16-bit keys (variant 16)
+    g.variant = 16;
     // col1 chunk staged per LDS fill: the whole row when it fits
     const int max_chunk = max_lds_bytes / (words * 4 + extra_col_bytes);
     g.chunk = cols < max_chunk ? cols : max_chunk;
@@ -1665,10 +1419,8 @@ SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes,
     // so wide workgroups are what fill the 32 wave slots (measured: 4 waves -1 %, 2 waves
     // +40 % time at cfg2)
     g.waves = waves ? waves : 8;
-    g.R = R ? R : 2;
-    if (g.variant == 32) {
-        g.split = 1;
-    } else if (split) {
+    g.R = R == 4 ? 4 : 2;
+    if (split) {
         g.split = split;
     } else {
         // Split the col1 scan across waves so the grid fills whole "rounds" of resident
@@ -1704,7 +1456,7 @@ hipError_t launch_search(SearchArgs a, const SearchGeometry& g, int words, bool 
     a.tiles_per_row = g.tiles_per_row;
     a.split = g.split;
     if (g.waves % g.split) return hipErrorInvalidValue;
-    if (a.out_f32 && (g.variant != 16 || !nodupes || (a.depth != 1 && a.depth != 2)))
+    if (a.out_f32 && (!nodupes || (a.depth != 1 && a.depth != 2)))
         return hipErrorInvalidValue;  // the fused agree epilogue exists for these only
     switch (words) {
         case 1: return launch_search_w<1>(a, nodupes, g, st);

@@ -54,7 +54,7 @@ struct SearchGeometry {
     int waves;              // waves per workgroup
     int R;                  // col0 per lane
     int tiles_per_row;
-    int variant;            // 16: packed 16-bit keys (default), 32: 32-bit keys
+    int variant;            // 16: packed 16-bit keys (the one VALU search)
     int split;              // packed variant: col1 split across waves of a workgroup (1, 2, 4, 8)
 };
 

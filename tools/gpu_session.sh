@@ -101,9 +101,6 @@ for step in "$@"; do
                 run diag${d}_${SC:-cfg2} 300 python tools/search_sweep.py --config ${SC:-cfg2} --variants ${SV:-0:0:0}
             done
             cp build/cur.so libbicos_amd/libbicos_amd.so ;;
-        sweep) run sweep 600 python tools/search_sweep.py --variants 16:2:8:2,18:2:8:2,16:2:8:1,18:2:8:1,18:4:8:2,17:2:8:2 ;;
-        sweep4) run sweep4 600 python tools/search_sweep.py --config cfg4 --variants 16:2:8:2,18:2:8:2,18:4:8:2 ;;
-        sweep1) run sweep1 600 python tools/search_sweep.py --config cfg1 --variants 32:1:4,32:2:4,16:2:4,16:4:4,16:2:2,16:2:1 ;;
         sweep8) run sweep8 600 python tools/search_sweep.py --rows 192 --variants 0:0:0:0,16:2:8:4,16:2:8:8,16:4:8:8 ;;
         sweep48) run sweep48 600 python tools/search_sweep.py --rows 384 --variants 0:0:0:0,16:2:8:2,16:2:8:4,16:2:8:8 && python tools/search_sweep.py --rows 768 --variants 0:0:0:0,16:2:8:1,16:2:8:2,16:2:8:4 && python tools/search_sweep.py --config cfg5 --rows 270 --variants 0:0:0:0,16:2:8:4,16:2:8:8 ;;
         sweep5) run sweep5 600 python tools/search_sweep.py --config cfg5 --rows 270 --variants 0:0:0:0,16:2:8:1,16:2:8:2,16:2:8:4 ;;

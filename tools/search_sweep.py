@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rows", type=int, default=0, help="row band size (0 = full frame)")
-    ap.add_argument("--variants", default="32:2:4,16:2:4,16:4:4,16:2:8,16:4:8,16:2:2,16:4:2")
+    ap.add_argument("--variants", default="0:0:0,16:2:8,16:4:8,16:2:4,16:4:4")
     ap.add_argument("--all-bits", action="store_true", help="no used-bits hint (all K-steps)")
     args = ap.parse_args()
     C = bench.CONFIGS[args.config]
