@@ -39,6 +39,12 @@
 #include <cstring>
 #include <type_traits>
 
+// 1: KEYS 2 reduces tiles in pairs (one lane-half exchange per two tiles); 0: per tile
+// (A/B builds, tools/build_alt.sh)
+#ifndef BICOS_MX_PAIRS
+#define BICOS_MX_PAIRS 1
+#endif
+
 namespace bicos_hip {
 
 namespace {
@@ -183,7 +189,9 @@ void search_mx_kernel(SearchArgs a) {
     const int tile = logical % a.tiles_per_row;
 
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    // wave-uniform, so the block loop's indices and addresses live in SGPRs (the SALU
+    // computes them; the VALU issue slots beside the MFMAs are the scarce resource)
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int h = lane >> 5;
     const int j = lane & 31;
     const int cols = a.cols;
@@ -211,7 +219,10 @@ void search_mx_kernel(SearchArgs a) {
         }
     }
 
-    uint32_t m1[T], m2[T];
+    // PAIRS (KEYS 2): the running first minima of tiles 2p / 2p+1 share register mp[p]
+    // (lanes 0-31 / 32-63: the halves that write those tiles), see block()
+    constexpr bool PAIRS = FREE && T % 2 == 0 && BICOS_MX_PAIRS;
+    uint32_t m1[T], m2[T], mp[T / 2 > 0 ? T / 2 : 1];
     int b2[T];  // KEYS 2: the base m2[t] is relative to (wave-uniform)
 #pragma unroll
     for (int t = 0; t < T; ++t) {
@@ -219,19 +230,23 @@ void search_mx_kernel(SearchArgs a) {
         m2[t] = XK ? XK_INF : 0u;
         b2[t] = 0;
     }
+#pragma unroll
+    for (int p = 0; p < (T / 2 > 0 ? T / 2 : 1); ++p) mp[p] = XK_INF;
 
     // row offset of accumulator register r in this lane half
     auto rrow = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; };
 
     v16f d[T], e[T];
-    auto products = [&](int t, const v4i* af, const v4i* an, const v16f& c1, const v16f& c2) {
-        d[t] = mfma_fp4(af[0], bf[t][0], c1);
+    // products of tile `tile` into accumulator slot `slot`
+    auto products = [&](int slot, const v4i* af, const v4i* an, const v16f& c1, const v16f& c2,
+                        int tile) {
+        d[slot] = mfma_fp4(af[0], bf[tile][0], c1);
 #pragma unroll
-        for (int s = 1; s < KS; ++s) d[t] = mfma_fp4(af[s], bf[t][s], d[t]);
+        for (int s = 1; s < KS; ++s) d[slot] = mfma_fp4(af[s], bf[tile][s], d[slot]);
         if constexpr (NODUPES && !XK) {
-            e[t] = mfma_fp4(an[0], bf[t][0], c2);
+            e[slot] = mfma_fp4(an[0], bf[tile][0], c2);
 #pragma unroll
-            for (int s = 1; s < KS; ++s) e[t] = mfma_fp4(an[s], bf[t][s], e[t]);
+            for (int s = 1; s < KS; ++s) e[slot] = mfma_fp4(an[s], bf[tile][s], e[slot]);
         }
     };
     // block at base B, the previous one at base bp (XK: the running minima move from bp's
@@ -326,6 +341,43 @@ void search_mx_kernel(SearchArgs a) {
             v4i af[KS], an[KS];
 #pragma unroll
             for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + 32 * b + j];
+#if !defined(BICOS_MX_DIAG)
+            if constexpr (FREE && PAIRS) {
+                // tiles in pairs (2p, 2p+1): ONE v_permlane32_swap of the two block minima
+                // leaves tile 2p's both-halves minimum in lanes 0-31 and tile 2p+1's in
+                // lanes 32-63 (swap: vdst lanes 32-63 <-> src lanes 0-31), where the pair's
+                // running first minima mp[p] live; one wave-uniform branch per pair, then a
+                // scalar test per tile of the ballot's halves
+                const uint32_t shift = (uint32_t)(B - bprev);
+#pragma unroll
+                for (int p = 0; p < T / 2; ++p) {
+                    products(0, af, an, c1, c2, 2 * p);
+                    products(1, af, an, c1, c2, 2 * p + 1);
+                    const uint32_t x = min16(d[0], KEY_NONE, 0u);
+                    const uint32_t y = min16(d[1], KEY_NONE, 0u);
+                    const auto sw = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+                    const uint32_t comb = min((uint32_t)sw[0], (uint32_t)sw[1]);
+                    const uint32_t ms = mp[p] - shift;
+                    const bool reach = comb <= (ms | XK_COL);  // cost <= running minimum cost
+                    mp[p] = min(ms, comb);
+                    const uint64_t bal = __builtin_amdgcn_ballot_w64(reach);
+                    // (halves as opaque SGPRs: left alone the compiler tests the upper one
+                    // with a 64-bit VALU compare)
+                    uint32_t lo = (uint32_t)bal, hi = (uint32_t)(bal >> 32);
+                    asm volatile("" : "+s"(lo), "+s"(hi));
+                    if (lo) {
+                        m2[2 * p] = min16(d[0], m2[2 * p] + (uint32_t)(B - b2[2 * p]), XK_COL);
+                        b2[2 * p] = B;
+                    }
+                    if (hi) {
+                        m2[2 * p + 1] = min16(d[1], m2[2 * p + 1] + (uint32_t)(B - b2[2 * p + 1]), XK_COL);
+                        b2[2 * p + 1] = B;
+                    }
+                }
+                bprev = B;
+                return;
+            }
+#endif
             if constexpr (NODUPES && !XK) {
 #pragma unroll
                 for (int s = 0; s < KS; ++s)
@@ -334,10 +386,10 @@ void search_mx_kernel(SearchArgs a) {
             }
             // tile t+1's products are issued before tile t's keys are reduced, so the MFMAs
             // overlap the reduction (and its branch) within the wave
-            products(0, af, an, c1, c2);
+            products(0, af, an, c1, c2, 0);
 #pragma unroll
             for (int t = 0; t < T; ++t) {
-                if (t + 1 < T) products(t + 1, af, an, c1, c2);
+                if (t + 1 < T) products(t + 1, af, an, c1, c2, t + 1);
                 reduce(t, B, bprev);
             }
             bprev = B;
@@ -390,7 +442,10 @@ void search_mx_kernel(SearchArgs a) {
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         if constexpr (FREE) m2[t] += (uint32_t)(bprev - b2[t]);  // into the last block's frame
-        m1[t] = min(m1[t], (uint32_t)__shfl_xor((int)m1[t], 32));
+        if constexpr (PAIRS)  // already merged; valid in the half that writes tile t
+            m1[t] = mp[t / 2];
+        else
+            m1[t] = min(m1[t], (uint32_t)__shfl_xor((int)m1[t], 32));
         if constexpr (NODUPES && XK) m2[t] = min(m2[t], (uint32_t)__shfl_xor((int)m2[t], 32));
         else if constexpr (NODUPES) m2[t] = max(m2[t], (uint32_t)__shfl_xor((int)m2[t], 32));
     }
