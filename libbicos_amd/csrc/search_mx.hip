@@ -44,6 +44,10 @@
 #ifndef BICOS_MX_PAIRS
 #define BICOS_MX_PAIRS 1
 #endif
+// 1: KEYS 2 with 2 tiles per wave runs the software-pipelined block loop
+#ifndef BICOS_MX_PIPE
+#define BICOS_MX_PIPE 1
+#endif
 
 namespace bicos_hip {
 
@@ -82,20 +86,18 @@ constexpr uint32_t XK_INF = 0x7F000000u;  // "no key yet"; stays huge under the 
 constexpr int XKF_K0 = 8160;
 constexpr int XKF_MAX_COLS = 8160;
 
-// nibble p of the result = bit p of `b` (b < 256): 1 -> 0x1
-__device__ __forceinline__ uint32_t spread8(uint32_t b) {
-    uint32_t t = (b | (b << 12)) & 0x000F000Fu;
-    t = (t | (t << 6)) & 0x03030303u;
-    return (t | (t << 3)) & 0x11111111u;
-}
-
-// 32 descriptor bits -> 32 FP4 elements (element 8q + p = nibble p of dword q = bit 8q + p)
-__device__ __forceinline__ v4i expand_bits(uint32_t x) {
+// 32 descriptor bits -> 32 FP4 elements through a byte table: byte q of dword m holds bits
+// 8q + 2m (low nibble) and 8q + 2m + 1 (high nibble), i.e. dword m = v_perm of the 4-entry
+// table `lut` (one byte per bit pair) selected by the pairs (x >> 2m) & 3 of every byte.
+// The order of the bits along K does not matter as long as both operands use the same
+// one; 4 v_perm + 7 shift/and per word instead of ~28 shift/or/and.
+constexpr uint32_t LUT_A = 0x22200200u;  // right (A): bit 1 -> 1.0 (0x2), 0 -> 0
+constexpr uint32_t LUT_B = 0xAAA22A22u;  // left (B): bit 1 -> -1.0 (0xA), 0 -> +1.0 (0x2)
+__device__ __forceinline__ v4i expand_bits(uint32_t x, uint32_t lut) {
     v4i r;
-    r[0] = (int)spread8(x & 0xFFu);
-    r[1] = (int)spread8((x >> 8) & 0xFFu);
-    r[2] = (int)spread8((x >> 16) & 0xFFu);
-    r[3] = (int)spread8(x >> 24);
+#pragma unroll
+    for (int m = 0; m < 4; ++m)
+        r[m] = (int)__builtin_amdgcn_perm(lut, lut, (x >> (2 * m)) & 0x03030303u);
     return r;
 }
 
@@ -213,15 +215,15 @@ void search_mx_kernel(SearchArgs a) {
             uint32_t x = 0;
             if (c0 < cols && w < WORDS) x = row0[(size_t)c0 * WORDS + w];
             if (WORDS == 8 && KS == 4 && w == 7) x &= 0x7FFFFFFFu;  // bit 255 masked (see below)
-            const v4i e = expand_bits(x);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) bf[t][s][q] = (int)(0x22222222u | ((uint32_t)e[q] << 3));
+            bf[t][s] = expand_bits(x, LUT_B);
         }
     }
 
     // PAIRS (KEYS 2): the running first minima of tiles 2p / 2p+1 share register mp[p]
     // (lanes 0-31 / 32-63: the halves that write those tiles), see block()
     constexpr bool PAIRS = FREE && T % 2 == 0 && BICOS_MX_PAIRS;
+    // one pair per wave: the block loop is software-pipelined (see the FREE chunk loop)
+    constexpr bool PIPE = PAIRS && T == 2 && BICOS_MX_PIPE;
     uint32_t m1[T], m2[T], mp[T / 2 > 0 ? T / 2 : 1];
     int b2[T];  // KEYS 2: the base m2[t] is relative to (wave-uniform)
 #pragma unroll
@@ -287,6 +289,34 @@ void search_mx_kernel(SearchArgs a) {
             if constexpr (NODUPES) m2[t] = max16(e[t], m2[t]);
         }
     };
+    int bprev = XK && !FREE ? -32 : 0;  // base of the previously reduced block
+    // KEYS 2, tiles in pairs (2p, 2p+1) for block base B (accumulators dx, dy): ONE
+    // v_permlane32_swap of the two block minima leaves tile 2p's both-halves minimum in
+    // lanes 0-31 and tile 2p+1's in lanes 32-63 (swap: vdst lanes 32-63 <-> src lanes 0-31),
+    // where the pair's running first minima mp[p] live; one wave-uniform branch per pair,
+    // then a scalar test per tile of the ballot's halves. The caller sets bprev = B after.
+    auto pair_reduce = [&](int p, int B, const v16f& dx, const v16f& dy) {
+        const uint32_t x = min16(dx, KEY_NONE, 0u);
+        const uint32_t y = min16(dy, KEY_NONE, 0u);
+        const auto sw = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+        const uint32_t comb = min((uint32_t)sw[0], (uint32_t)sw[1]);
+        const uint32_t ms = mp[p] - (uint32_t)(B - bprev);
+        const bool reach = comb <= (ms | XK_COL);  // cost <= running minimum cost
+        mp[p] = min(ms, comb);
+        const uint64_t bal = __builtin_amdgcn_ballot_w64(reach);
+        // (halves as opaque SGPRs: left alone the compiler tests the upper one with a 64-bit
+        // VALU compare)
+        uint32_t lo = (uint32_t)bal, hi = (uint32_t)(bal >> 32);
+        asm volatile("" : "+s"(lo), "+s"(hi));
+        if (lo) {
+            m2[2 * p] = min16(dx, m2[2 * p] + (uint32_t)(B - b2[2 * p]), XK_COL);
+            b2[2 * p] = B;
+        }
+        if (hi) {
+            m2[2 * p + 1] = min16(dy, m2[2 * p + 1] + (uint32_t)(B - b2[2 * p + 1]), XK_COL);
+            b2[2 * p + 1] = B;
+        }
+    };
     // XK: the C of every block (col1 % 32 only)
     v16f cx;
 #pragma unroll
@@ -297,7 +327,6 @@ void search_mx_kernel(SearchArgs a) {
     // FREE: chunks downwards from the one holding the workgroup's highest col0
     int cstart = 0;
     if constexpr (FREE) cstart = min(cols - 1, (tile + 1) * waves * T * 32 - 1) / chunk;
-    int bprev = XK && !FREE ? -32 : 0;  // base of the previously reduced block
     for (int k = 0; k < nchunks; ++k) {
         int ci = FREE ? cstart - k : k;
         if (ci < 0) ci += nchunks;
@@ -317,11 +346,7 @@ void search_mx_kernel(SearchArgs a) {
                 uint32_t x = 0;
                 if (c1 < cols && w < WORDS) x = row1[(size_t)c1 * WORDS + w];
                 if (WORDS == 8 && KS == 4 && w == 7) x &= 0x7FFFFFFFu;
-                const v4i ex = expand_bits(x);
-                v4i v;
-#pragma unroll
-                for (int q = 0; q < 4; ++q) v[q] = ex[q] << 1;  // 0x1 -> 0x2 (1.0)
-                lds_mx[w * chunk + c] = v;
+                lds_mx[w * chunk + c] = expand_bits(x, LUT_A);
             }
         }
         if (expand) __syncthreads();
@@ -343,36 +368,11 @@ void search_mx_kernel(SearchArgs a) {
             for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + 32 * b + j];
 #if !defined(BICOS_MX_DIAG)
             if constexpr (FREE && PAIRS) {
-                // tiles in pairs (2p, 2p+1): ONE v_permlane32_swap of the two block minima
-                // leaves tile 2p's both-halves minimum in lanes 0-31 and tile 2p+1's in
-                // lanes 32-63 (swap: vdst lanes 32-63 <-> src lanes 0-31), where the pair's
-                // running first minima mp[p] live; one wave-uniform branch per pair, then a
-                // scalar test per tile of the ballot's halves
-                const uint32_t shift = (uint32_t)(B - bprev);
 #pragma unroll
                 for (int p = 0; p < T / 2; ++p) {
                     products(0, af, an, c1, c2, 2 * p);
                     products(1, af, an, c1, c2, 2 * p + 1);
-                    const uint32_t x = min16(d[0], KEY_NONE, 0u);
-                    const uint32_t y = min16(d[1], KEY_NONE, 0u);
-                    const auto sw = __builtin_amdgcn_permlane32_swap(x, y, false, false);
-                    const uint32_t comb = min((uint32_t)sw[0], (uint32_t)sw[1]);
-                    const uint32_t ms = mp[p] - shift;
-                    const bool reach = comb <= (ms | XK_COL);  // cost <= running minimum cost
-                    mp[p] = min(ms, comb);
-                    const uint64_t bal = __builtin_amdgcn_ballot_w64(reach);
-                    // (halves as opaque SGPRs: left alone the compiler tests the upper one
-                    // with a 64-bit VALU compare)
-                    uint32_t lo = (uint32_t)bal, hi = (uint32_t)(bal >> 32);
-                    asm volatile("" : "+s"(lo), "+s"(hi));
-                    if (lo) {
-                        m2[2 * p] = min16(d[0], m2[2 * p] + (uint32_t)(B - b2[2 * p]), XK_COL);
-                        b2[2 * p] = B;
-                    }
-                    if (hi) {
-                        m2[2 * p + 1] = min16(d[1], m2[2 * p + 1] + (uint32_t)(B - b2[2 * p + 1]), XK_COL);
-                        b2[2 * p + 1] = B;
-                    }
+                    pair_reduce(p, B, d[0], d[1]);
                 }
                 bprev = B;
                 return;
@@ -410,6 +410,44 @@ void search_mx_kernel(SearchArgs a) {
             if (partial) partial_block(cc);
             // full blocks downwards from the one holding the wave's highest col0 (clamped)
             const int sb = max(0, min(nfull - 1, (c0_wave + 32 * T - 1 - base) / 32));
+#if !defined(BICOS_MX_DIAG)
+            if constexpr (PIPE) {
+                // software pipeline over the blocks (one tile pair per wave): the products of
+                // block i+1 are issued before block i is reduced, so the wave's MFMAs stay in
+                // flight during its own key reduction (accumulator sets A / B alternate)
+                v16f dA[2], dB[2];
+                int BA = 0, BB = 0;
+                auto issue = [&](int i, v16f* dd) {
+                    int b = sb - i;
+                    if (b < 0) b += nfull;
+                    v4i af[KS];
+#pragma unroll
+                    for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + 32 * b + j];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) {
+                        dd[u] = mfma_fp4(af[0], bf[u][0], cc);
+#pragma unroll
+                        for (int s = 1; s < KS; ++s) dd[u] = mfma_fp4(af[s], bf[u][s], dd[u]);
+                    }
+                    return base + 32 * b;
+                };
+                auto finish = [&](int B, const v16f* dd) {
+                    pair_reduce(0, B, dd[0], dd[1]);
+                    bprev = B;
+                };
+                if (nfull > 0) {
+                    BA = issue(0, dA);
+                    for (int i = 0;;) {
+                        if (i + 1 < nfull) BB = issue(i + 1, dB);
+                        finish(BA, dA);
+                        if (++i >= nfull) break;
+                        if (i + 1 < nfull) BA = issue(i + 1, dA);
+                        finish(BB, dB);
+                        if (++i >= nfull) break;
+                    }
+                }
+            } else
+#endif
             for (int i = 0; i < nfull; ++i) {
                 int b = sb - i;
                 if (b < 0) b += nfull;
