@@ -112,13 +112,24 @@ def mx_search() -> bool:
     return os.environ.get("BICOS_SEARCH", "") != "valu"
 
 
-def mx_flops(rows: int, W: int, words: int, cfg: dict):
+def mx_ksteps(words: int, bits: int) -> int:
+    """64-bit K-steps the matrix-core search multiplies (search_mx.hip
+    search_mx_geometry): all of the descriptor, except 3 of 4 for 256-bit descriptors
+    whose used bits (the transform's 4n-5 / n^2-2n+3) fit in 192."""
+    ks = max(1, words // 2)
+    if words == 8 and 0 < bits <= 192:
+        ks = 3
+    return ks
+
+
+def mx_flops(rows: int, W: int, words: int, cfg: dict, bits: int = 0):
     """(algorithmic, executed) FLOPs of the matrix-core search per launch. Each Hamming
-    pair is a K-long dot product, K = descriptor bits (2K FLOPs); the MFMA executes K
-    padded to its 64-bit steps. Consistency runs the forward and the reverse search."""
+    pair is a K-long dot product, K = descriptor bits (2K FLOPs); the MFMA executes the
+    K-steps that hold used bits (mx_ksteps). Consistency runs the forward and the reverse
+    search."""
     passes = 2 if cfg.get("variant", 0) == 1 else 1
     pairs = search_pairs(rows, W, cfg) * passes
-    return pairs * 2 * 32 * words, pairs * 2 * 64 * max(1, words // 2)
+    return pairs * 2 * 32 * words, pairs * 2 * 64 * mx_ksteps(words, bits)
 
 
 def mx_key_pair_peak(words: int, cfg: dict) -> float:
@@ -377,8 +388,10 @@ def main():
         if fused_agree:
             eng.search_agree(d0, d1, s0, s1, words, mcfg.nxcorr_threshold, minvar_scaled=mv)
         else:
-            eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw)
+            # with the used-bits hint the pipeline passes (engine.cpp match_device)
+            eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw, bits=ubits)
 
+    ubits = device.used_bits(n, mcfg.mode)
     search_launch()  # warm
     ev[0].record(st)
     for _ in range(args.kernel_reps):
@@ -418,7 +431,7 @@ def main():
     kname = "search_mx_kernel" if mx else ("search_lr_kernel" if cons else "search16_kernel")
     traffic = load_traffic(kname, rows, W) if args.config == "cfg2" and rows == H else None
     if mx:
-        alg_flops, exe_flops = mx_flops(rows, W, words, C["cfg"])
+        alg_flops, exe_flops = mx_flops(rows, W, words, C["cfg"], ubits)
         achieved_tf = alg_flops / t_search / 1e12
         kpeak = mx_key_pair_peak(words, C["cfg"]) / 1e9
         evaluated = pairs * (2 if cons else 1)
