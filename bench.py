@@ -106,6 +106,17 @@ def search_ops(rows: int, W: int, words: int, cfg: dict) -> float:
     return search_pairs(rows, W, cfg) * (2 * words + (3 if dupes else 2))
 
 
+def subpixel_steps(step: float) -> int:
+    """x values of the reference's refine loop, for (float x = -1; x <= 1; x += step)
+    accumulated in float32 (agree.hpp:122; engine.cpp subpixel_steps)."""
+    import numpy as np
+    x, k, st = np.float32(-1.0), 0, np.float32(step)
+    while x <= np.float32(1.0):
+        k += 1
+        x = np.float32(x + st)
+    return k
+
+
 def mx_search() -> bool:
     """The pipeline's search runs on the matrix cores unless BICOS_SEARCH=valu
     (engine.cpp use_mx)."""
@@ -491,6 +502,24 @@ def main():
                 "nominal_peak_Tops": round(VALU_NOMINAL_TOPS, 1),
                 "ops_model": "one pass over the cost matrix, 32-bit keys: 2w+3 (2w+2) lane-ops per pair",
             },
+        }
+    if stage == "subpixel":
+        # the refine is fp32-VALU work: per valid pixel and x step, n x (quadratic 5 +
+        # round/wrap 3 + mean sum 1 + centre 1 + two fma) = 12n lane-ops, plus the step's NXC
+        # (correctly rounded sqrt + division + argmax, ~30)
+        xs = subpixel_steps(mc["subpixel_step"])
+        sp_ops = rows * W * valid * xs * (12 * n + 30)
+        roof["subpixel"] = {
+            "bound": "valu (fp32)",
+            "x_steps": xs,
+            "lane_ops": sp_ops,
+            "ops_model": "per valid px and x step: 12 x n (interp 5, round/wrap 3, sum 1, "
+                         "centre 1, fma 2) + 30 (NXC sqrt/div/argmax)",
+            "achieved_Tops": round(sp_ops / t_agree / 1e12, 2),
+            "peak_Tops": VALU_FULL_TOPS,
+            "frac": round(sp_ops / t_agree / 1e12 / VALU_FULL_TOPS, 4),
+            "ms": round(t_agree * 1e3, 4),
+            "peak_source": "profiles/valu_rates_r01.jsonl (full-rate fp32/int ops, measured)",
         }
     roof.update({
         "hbm": {

@@ -6,7 +6,7 @@
 //   search_lr_kernel    the same, Consistency's forward + reverse minima in one pass
 //   consistency_kernel  left-right check      (reference include/impl/cpu/bicos.hpp:99-106)
 //   agree_kernel        NXC filter            (reference include/impl/cpu/agree.hpp:28-93)
-//   subpixel_kernel     NXC + quadratic refine(reference include/impl/cpu/agree.hpp:95-191)
+//   (subpixel_kernel, the NXC + quadratic refine of agree.hpp:95-191: subpixel.hpp)
 //
 // Layouts in HBM (see DESIGN.md "Data layout"):
 //   image stack   planar [n][rows][row_pitch] of u8/u16 (the reference's vector<Image>)
@@ -19,6 +19,7 @@
 // division and sqrt), fmaf exactly where the reference calls std::fmaf.
 #include "kernels.hpp"
 #include "nxc.hpp"
+#include "stack.hpp"
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -50,23 +51,8 @@ using nxc::ld;
 using nxc::fma_p;
 using nxc::div_p;
 using nxc::sqrt_p;
+using nxc::nxcorr_dev;
 
-// Raw buffer loads of an image stack: 128-bit resource built from uniform values, uniform
-// (SGPR) byte offset of the plane/row, 32-bit per-lane byte offset -- no VALU address math
-// per load (guide T8). Stacks are limited to < 4 GiB (checked by the engine).
-template <typename TIn>
-struct StackReader {
-    __amdgpu_buffer_rsrc_t r;
-    __device__ __forceinline__ StackReader(const void* base, uint32_t bytes)
-        : r(__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes,
-                                               0x00020000)) {}
-    __device__ __forceinline__ uint32_t operator()(uint32_t lane_elem, uint32_t uniform_elem) const {
-        if constexpr (sizeof(TIn) == 1)
-            return __builtin_amdgcn_raw_buffer_load_b8(r, lane_elem, uniform_elem, 0);
-        else
-            return __builtin_amdgcn_raw_buffer_load_b16(r, lane_elem * 2u, uniform_elem * 2u, 0);
-    }
-};
 
 // ------------------------------------------------------------------ transform
 
@@ -833,31 +819,6 @@ __global__ __launch_bounds__(256) void consistency_kernel(ConsistencyArgs a) {
 
 // fma_p / div_p / sqrt_p (IEEE, correctly rounded): nxc.hpp
 
-// nxcorr (agree.hpp:28-51): means from exact integer sums (< 2^24, identical to the
-// reference's sequential float sums); centred samples, three fma chains in t order,
-// IEEE sqrt and division. TPrec = double is the CUDA build's Precision::DOUBLE
-// (agree.cuh:35-65), which has no CPU counterpart in the reference.
-template <typename TIn, typename TPrec>
-__device__ __forceinline__ TPrec nxcorr_dev(const TIn* __restrict__ p0, const TIn* __restrict__ p1,
-                                           size_t pp, int n, bool has_minvar, TPrec minvar) {
-    uint32_t s0 = 0, s1 = 0;
-    for (int t = 0; t < n; ++t) {
-        s0 += ld(p0 + t * pp);
-        s1 += ld(p1 + t * pp);
-    }
-    const TPrec m0 = div_p((TPrec)s0, (TPrec)n);
-    const TPrec m1 = div_p((TPrec)s1, (TPrec)n);
-    TPrec cov = 0, v0 = 0, v1 = 0;
-    for (int t = 0; t < n; ++t) {
-        const TPrec x0 = (TPrec)ld(p0 + t * pp) - m0;
-        const TPrec x1 = (TPrec)ld(p1 + t * pp) - m1;
-        cov = fma_p(x0, x1, cov);
-        v0 = fma_p(x0, x0, v0);
-        v1 = fma_p(x1, x1, v1);
-    }
-    if (has_minvar && (v0 < minvar || v1 < minvar)) return (TPrec)-1;
-    return div_p(cov, sqrt_p(v0 * v1));
-}
 
 // agree (agree.hpp:53-93) fused with the float conversion of cpu.cpp:88-93 and the NaN
 // initialisation of the correlation map (cpu.cpp:78-81): writes every output pixel.
@@ -888,23 +849,6 @@ __global__ __launch_bounds__(256) void agree_kernel(AgreeArgs a) {
     if (a.corrmap) ((TPrec*)a.corrmap)[o] = corr;
 }
 
-// (column tile, row) of a (tiles x rows) grid, remapped so that each XCD gets a run of
-// whole rows: workgroups are dispatched round-robin over the 8 XCDs in linear order, so
-// without this neighbouring column tiles land on different XCDs and the right-image
-// windows they share (col - d, col1 +- 1) are fetched into two L2s.
-__device__ __forceinline__ void xcd_rows(int& tile, int& row) {
-    const int gx = gridDim.x;
-    const int nwg = gx * gridDim.y;
-    if (nwg % 8) {
-        tile = blockIdx.x;
-        row = blockIdx.y;
-        return;
-    }
-    const int bid = blockIdx.y * gx + blockIdx.x;
-    const int logical = (bid % 8) * (nwg / 8) + bid / 8;
-    tile = logical % gx;
-    row = logical / gx;
-}
 
 // agree with the 2n samples loaded once into registers (MAXN >= n), the same arithmetic
 // and output contract as agree_kernel.
@@ -1071,185 +1015,7 @@ __global__ __launch_bounds__(256) void agree_lds_kernel(AgreeArgs a) {
     if (a.corrmap) ((TPrec*)a.corrmap)[o] = corr;
 }
 
-// (TIn)roundevenf(A x^2 + B x + C) as a float (agree.cuh:221-236 / agree.hpp:140-150):
-// adding 1.5*2^23 rounds v to the nearest even integer k (|v| < 2^22 for 8/16-bit data)
-// and leaves k's two's-complement low bits in the mantissa, so the low byte/short of the
-// sum's bits IS (TIn)(int)k, the reference's wrap through int32. It goes back to float
-// exactly as (2^23 | low bits) - 2^23; the sum's top byte is always 0x4B, so that is one
-// full-rate AND with 0x4B0000FF (0x4B00FFFF) and a subtract, instead of the quarter-rate
-// v_cvt_f32_ubyte0 (tools/valu_peak.hip, op 19).
-constexpr float RND_MAGIC = 0x1.8p23f;
 
-// (float)k for |k| < 2^22, exactly: full-rate integer add + float subtract
-__device__ __forceinline__ float small_int_to_float(int k) {
-    uint32_t b = 0x4B400000u + (uint32_t)k;
-    asm("" : "+v"(b));  // keep LLVM from folding this back into v_cvt_f32_i32
-    return __uint_as_float(b) - RND_MAGIC;
-}
-template <typename TIn>
-constexpr uint32_t wrap_mask() { return sizeof(TIn) == 1 ? 0x4B0000FFu : 0x4B00FFFFu; }
-
-template <typename TIn>
-__device__ __forceinline__ float interp_wrapped(float A, float B, float C, float x) {
-    const float ax = A * x;
-    const float v = (ax * x + B * x) + C;
-    uint32_t bits = __float_as_uint(v + RND_MAGIC) & wrap_mask<TIn>();
-    asm("" : "+v"(bits));  // keep LLVM from folding this back into a cvt
-    return __uint_as_float(bits) - 0x1p23f;
-}
-
-// agree_subpixel (agree.hpp:95-191). MAXN >= n bounds the per-lane register arrays
-// (static indices only). Slots t < LO (the smallest n routed to this bucket) are always
-// live; slots LO <= t < MAXN beyond n are padded with exact no-ops: A = B = C = 0 gives
-// an interpolated 0 (sum unchanged), D0 = 0 and x1 = 0 leave both fma chains unchanged
-// (neither accumulator is ever -0). The quadratic is float in both precisions.
-//
-// The x loop is software-pipelined: one pass over t finishes step k (x1 = IV - m1 and the
-// in-order cov / var fma chains) and interpolates step k+1 into the same IV registers, so
-// every chain op has independent interpolation work beside it and the register footprint
-// is that of one step. nsteps is the host's count of x = -1, -1+step, ... <= 1, accumulated
-// in float exactly as the reference's loop (engine.cpp subpixel_steps).
-template <typename TIn, typename TPrec, int MAXN, int LO>
-__global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
-    int tile, row;
-    xcd_rows(tile, row);
-    const int col = tile * 256 + threadIdx.x;
-    if (col >= a.cols) return;
-    const size_t o = (size_t)row * a.cols + col;
-    const int n = LO == MAXN ? MAXN : a.n;
-    const size_t pp = a.plane_pitch;
-    const int d = a.raw[(size_t)row * a.raw_pitch + col];
-    const TPrec minvar = (TPrec)a.minvar;
-    float out = __builtin_nanf("");
-    TPrec corr = (TPrec)__builtin_nan("");
-    const int col1 = col - d;
-    if (d != INVALID_I16 && col1 >= 0 && col1 < a.cols) {
-        const TIn* s0 = (const TIn*)a.stack0 + (size_t)row * a.row_pitch + col;
-        const TIn* s1 = (const TIn*)a.stack1 + (size_t)row * a.row_pitch + col1;
-        if (col1 == 0 || col1 == a.cols - 1) {
-            corr = nxcorr_dev<TIn, TPrec>(s0, s1, pp, n, a.has_minvar, minvar);
-            if (!(corr < (TPrec)a.threshold)) out = (float)d;
-        } else {
-            const StackReader<TIn> rd0(a.stack0, a.stack_bytes), rd1(a.stack1, a.stack_bytes);
-            const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
-            // left: mean, centred samples and variance are the same for every x
-            // padded slots re-read plane 0 (in bounds) and are zeroed; int -> float via
-            // small_int_to_float (two full-rate ops instead of a quarter-rate v_cvt_f32_*)
-            TPrec D0[MAXN];
-            float A[MAXN], B[MAXN], C[MAXN];
-            uint32_t s = 0;
-#pragma unroll
-            for (int t = 0; t < MAXN; ++t) {
-                const bool live = t < LO || t < n;
-                const uint32_t po = rowoff + (live ? (uint32_t)(t * pp) : 0u);
-                const uint32_t l = rd0((uint32_t)col, po);
-                const int y0 = (int)rd1((uint32_t)(col1 - 1), po);
-                const int y1 = (int)rd1((uint32_t)col1, po);
-                const int y2 = (int)rd1((uint32_t)(col1 + 1), po);
-                // 0.5f * ( y0 - 2.0f * y1 + y2) ; 0.5f * (-y0 + y2) ; y1 -- exact on integers
-                // of this size, so formed in int and converted once
-                A[t] = live ? 0.5f * small_int_to_float(y0 - 2 * y1 + y2) : 0.f;
-                B[t] = live ? 0.5f * small_int_to_float(y2 - y0) : 0.f;
-                C[t] = live ? small_int_to_float(y1) : 0.f;
-                D0[t] = live ? (TPrec)small_int_to_float((int)l) : (TPrec)0;
-                s += live ? l : 0u;
-            }
-            const TPrec m0 = div_p((TPrec)s, (TPrec)n);
-            TPrec v0 = 0;
-#pragma unroll
-            for (int t = 0; t < MAXN; ++t) {
-                const bool live = t < LO || t < n;
-                D0[t] = live ? D0[t] - m0 : (TPrec)0;
-                v0 = fma_p(D0[t], D0[t], v0);
-            }
-            const bool v0_low = a.has_minvar && v0 < minvar;
-
-            float best_x = 0.f;
-            TPrec best = -1;
-            const float step = a.step;
-            float x = -1.f;
-            // cov / var of step x, then the reference's argmax (first maximum wins)
-            auto finish = [&](TPrec cov, TPrec v1) {
-                TPrec nxc;
-                if (v0_low || (a.has_minvar && v1 < minvar))
-                    nxc = -1;
-                else
-                    nxc = div_p(cov, sqrt_p(v0 * v1));
-                if (best < nxc) {
-                    best_x = x;
-                    best = nxc;
-                }
-            };
-            float IV[MAXN];
-            float sf[4] = {0.f, 0.f, 0.f, 0.f};  // exact in any order: integers < 2^24
-            if constexpr (MAXN <= 40) {
-                // Software-pipelined: one pass over t finishes step k (x1 = IV - m1 and the
-                // in-order fma chains) and interpolates step k+1 into the same registers.
-#pragma unroll
-                for (int t = 0; t < MAXN; ++t) {
-                    IV[t] = interp_wrapped<TIn>(A[t], B[t], C[t], x);
-                    sf[t & 3] += IV[t];
-                }
-                for (int k = 0; k < a.nsteps; ++k) {
-                    const TPrec m1 = div_p((TPrec)((sf[0] + sf[1]) + (sf[2] + sf[3])), (TPrec)n);
-                    const float xn = x + step;
-                    TPrec cov = 0, v1 = 0;
-                    // two copies of the body: a wave-uniform test inside the unrolled t loop
-                    // becomes one scalar branch per slot and breaks the schedule (measured 3x)
-                    if (k + 1 < a.nsteps) {
-#pragma unroll
-                        for (int t = 0; t < MAXN; ++t) {
-                            TPrec x1 = (TPrec)IV[t] - m1;
-                            if (t >= LO) x1 = t < n ? x1 : (TPrec)0;
-                            cov = fma_p(D0[t], x1, cov);
-                            v1 = fma_p(x1, x1, v1);
-                            IV[t] = interp_wrapped<TIn>(A[t], B[t], C[t], xn);
-                        }
-                        sf[0] = sf[1] = sf[2] = sf[3] = 0.f;
-#pragma unroll
-                        for (int t = 0; t < MAXN; ++t) sf[t & 3] += IV[t];
-                    } else {
-#pragma unroll
-                        for (int t = 0; t < MAXN; ++t) {
-                            TPrec x1 = (TPrec)IV[t] - m1;
-                            if (t >= LO) x1 = t < n ? x1 : (TPrec)0;
-                            cov = fma_p(D0[t], x1, cov);
-                            v1 = fma_p(x1, x1, v1);
-                        }
-                    }
-                    finish(cov, v1);
-                    x = xn;
-                }
-            } else {
-                // One wave/SIMD: the arrays already overflow into AGPRs, so keep IV dead
-                // across the loop's back edge (interpolate at the top of each step).
-                for (int k = 0; k < a.nsteps; ++k) {
-                    sf[0] = sf[1] = sf[2] = sf[3] = 0.f;
-#pragma unroll
-                    for (int t = 0; t < MAXN; ++t) {
-                        IV[t] = interp_wrapped<TIn>(A[t], B[t], C[t], x);
-                        sf[t & 3] += IV[t];
-                    }
-                    const TPrec m1 = div_p((TPrec)((sf[0] + sf[1]) + (sf[2] + sf[3])), (TPrec)n);
-                    TPrec cov = 0, v1 = 0;
-#pragma unroll
-                    for (int t = 0; t < MAXN; ++t) {
-                        TPrec x1 = (TPrec)IV[t] - m1;
-                        if (t >= LO) x1 = t < n ? x1 : (TPrec)0;
-                        cov = fma_p(D0[t], x1, cov);
-                        v1 = fma_p(x1, x1, v1);
-                    }
-                    finish(cov, v1);
-                    x += step;
-                }
-            }
-            corr = best;
-            if (!(best < (TPrec)a.threshold)) out = (float)d - best_x;
-        }
-    }
-    ((float*)a.out)[o] = out;
-    if (a.corrmap) ((TPrec*)a.corrmap)[o] = corr;
-}
 
 // ------------------------------------------------------------------- dispatch
 
@@ -1329,30 +1095,6 @@ hipError_t launch_search_w(const SearchArgs& a, bool nodupes, const SearchGeomet
     return nodupes ? launch_search_n<WORDS, true>(a, g, st) : launch_search_n<WORDS, false>(a, g, st);
 }
 
-template <typename TIn, typename TPrec, int MAXN, int LO>
-hipError_t launch_subpixel_m(const AgreeArgs& a, hipStream_t st) {
-    dim3 grid((a.cols + 255) / 256, a.rows);
-    if (a.n == MAXN)
-        hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN, MAXN>), grid, dim3(256), 0, st, a);
-    else
-        hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN, LO>), grid, dim3(256), 0, st, a);
-    return hipGetLastError();
-}
-
-template <typename TIn, typename TPrec>
-hipError_t launch_subpixel_t(const AgreeArgs& a, hipStream_t st) {
-    const int n = a.n;
-    if (a.nsteps < 1) return hipErrorInvalidValue;
-    if (n <= 8) return launch_subpixel_m<TIn, TPrec, 8, 2>(a, st);
-    if (n <= 16) return launch_subpixel_m<TIn, TPrec, 16, 9>(a, st);
-    if (n <= 24) return launch_subpixel_m<TIn, TPrec, 24, 17>(a, st);
-    if (n <= 33) return launch_subpixel_m<TIn, TPrec, 33, 25>(a, st);
-    if (n <= 40) return launch_subpixel_m<TIn, TPrec, 40, 34>(a, st);
-    if (n <= 48) return launch_subpixel_m<TIn, TPrec, 48, 41>(a, st);
-    if (n <= 56) return launch_subpixel_m<TIn, TPrec, 56, 49>(a, st);
-    if (n <= 65) return launch_subpixel_m<TIn, TPrec, 65, 57>(a, st);
-    return hipErrorInvalidValue;
-}
 
 template <typename TIn, typename TPrec, int MAXN>
 hipError_t launch_agree_m(const AgreeArgs& a, hipStream_t st) {
@@ -1537,15 +1279,6 @@ hipError_t launch_agree(const AgreeArgs& a, int depth, bool dbl, hipStream_t st)
     if (depth == 1)
         return dbl ? launch_agree_t<uint8_t, double>(a, st) : launch_agree_t<uint8_t, float>(a, st);
     return dbl ? launch_agree_t<uint16_t, double>(a, st) : launch_agree_t<uint16_t, float>(a, st);
-}
-
-hipError_t launch_subpixel(const AgreeArgs& a, int depth, bool dbl, hipStream_t st) {
-    if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
-    if (depth == 1)
-        return dbl ? launch_subpixel_t<uint8_t, double>(a, st)
-                   : launch_subpixel_t<uint8_t, float>(a, st);
-    return dbl ? launch_subpixel_t<uint16_t, double>(a, st)
-               : launch_subpixel_t<uint16_t, float>(a, st);
 }
 
 }  // namespace bicos_hip

@@ -122,5 +122,7 @@ hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool n
                             hipStream_t st);
 hipError_t launch_agree(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
 hipError_t launch_subpixel(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
+// n > 40 (subpixel_wide.hip); launch_subpixel dispatches to it
+hipError_t launch_subpixel_wide(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
 
 }  // namespace bicos_hip

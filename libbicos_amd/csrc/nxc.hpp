@@ -43,6 +43,32 @@ __device__ __forceinline__ float sqrt_p(float x) {
 }
 __device__ __forceinline__ double sqrt_p(double a) { return __dsqrt_rn(a); }
 
+// nxcorr (agree.hpp:28-51): means from exact integer sums (< 2^24, identical to the
+// reference's sequential float sums); centred samples, three fma chains in t order,
+// IEEE sqrt and division. TPrec = double is the CUDA build's Precision::DOUBLE
+// (agree.cuh:35-65), which has no CPU counterpart in the reference.
+template <typename TIn, typename TPrec>
+__device__ __forceinline__ TPrec nxcorr_dev(const TIn* __restrict__ p0, const TIn* __restrict__ p1,
+                                           size_t pp, int n, bool has_minvar, TPrec minvar) {
+    uint32_t s0 = 0, s1 = 0;
+    for (int t = 0; t < n; ++t) {
+        s0 += ld(p0 + t * pp);
+        s1 += ld(p1 + t * pp);
+    }
+    const TPrec m0 = div_p((TPrec)s0, (TPrec)n);
+    const TPrec m1 = div_p((TPrec)s1, (TPrec)n);
+    TPrec cov = 0, v0 = 0, v1 = 0;
+    for (int t = 0; t < n; ++t) {
+        const TPrec x0 = (TPrec)ld(p0 + t * pp) - m0;
+        const TPrec x1 = (TPrec)ld(p1 + t * pp) - m1;
+        cov = fma_p(x0, x1, cov);
+        v0 = fma_p(x0, x0, v0);
+        v1 = fma_p(x1, x1, v1);
+    }
+    if (has_minvar && (v0 < minvar || v1 < minvar)) return (TPrec)-1;
+    return div_p(cov, sqrt_p(v0 * v1));
+}
+
 // The agree of R pixels of one row at once (agree.hpp:53-93 with nxcorr agree.hpp:28-51 in
 // single precision): pixel r is column c0[r] of the left row, matched to column best[r] of
 // the right row; `in[r]` = the pixel exists, `live[r]` = its search result is valid (then

@@ -1,0 +1,36 @@
+// subpixel.hip -- the subpixel refine for stacks of up to 40 images, and the dispatch by
+// stack depth (launch_subpixel). Built with -fno-slp-vectorize (Makefile): the kernel is
+// VALU-issue-bound, and the packed f32 ops the SLP vectoriser forms (v_pk_mul/add/fma_f32)
+// issue in two cycles for their two values while their operand pairs cost extra v_mov;
+// scalar fp32 is 6-17 % faster for n <= 33. Deeper stacks (one wave per
+// SIMD, arrays past 256 registers) run the SLP build: subpixel_wide.hip.
+#include "subpixel.hpp"
+
+namespace bicos_hip {
+
+namespace {
+
+template <typename TIn, typename TPrec>
+hipError_t launch_subpixel_t(const AgreeArgs& a, int depth, bool dbl, hipStream_t st) {
+    const int n = a.n;
+    if (n <= 8) return launch_subpixel_m<TIn, TPrec, 8, 2>(a, st);
+    if (n <= 16) return launch_subpixel_m<TIn, TPrec, 16, 9>(a, st);
+    if (n <= 24) return launch_subpixel_m<TIn, TPrec, 24, 17>(a, st);
+    if (n <= 33) return launch_subpixel_m<TIn, TPrec, 33, 25>(a, st);
+    if (n <= 40) return launch_subpixel_m<TIn, TPrec, 40, 34>(a, st);
+    return launch_subpixel_wide(a, depth, dbl, st);
+}
+
+}  // namespace
+
+hipError_t launch_subpixel(const AgreeArgs& a, int depth, bool dbl, hipStream_t st) {
+    if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
+    if (a.nsteps < 1) return hipErrorInvalidValue;
+    if (depth == 1)
+        return dbl ? launch_subpixel_t<uint8_t, double>(a, depth, dbl, st)
+                   : launch_subpixel_t<uint8_t, float>(a, depth, dbl, st);
+    return dbl ? launch_subpixel_t<uint16_t, double>(a, depth, dbl, st)
+               : launch_subpixel_t<uint16_t, float>(a, depth, dbl, st);
+}
+
+}  // namespace bicos_hip
