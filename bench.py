@@ -461,6 +461,9 @@ def main():
             "algorithmic_bytes": search_bytes,
             "algorithmic_flops": alg_flops,
             "executed_flops": exe_flops,
+            # the K-steps the MFMA actually multiplies (256-bit descriptors of <= 192 used
+            # bits: 3 of 4) -- the same time against the executed work
+            "executed_frac": round(exe_flops / t_search / 1e12 / MFMA_FP4_DENSE_TFLOPS, 4),
             "pairs_per_launch": evaluated,
             "ms_per_launch": round(t_search * 1e3, 4),
             "peak_model": "dense FP4 MFMA peak (MI355X_MICROARCH.md); algorithmic FLOPs = "
