@@ -48,6 +48,10 @@
 #ifndef BICOS_MX_PIPE
 #define BICOS_MX_PIPE 1
 #endif
+// 1: XK searches prefetch the next block's A fragments (block_pf)
+#ifndef BICOS_MX_PREFETCH
+#define BICOS_MX_PREFETCH 1
+#endif
 
 namespace bicos_hip {
 
@@ -224,6 +228,11 @@ void search_mx_kernel(SearchArgs a) {
     constexpr bool PAIRS = FREE && T % 2 == 0 && BICOS_MX_PAIRS;
     // one pair per wave: the block loop is software-pipelined (see the FREE chunk loop)
     constexpr bool PIPE = PAIRS && T == 2 && BICOS_MX_PIPE;
+    // XK full blocks: the next block's A fragments are read while this one is reduced.
+    // Only where the registers allow (paired NoDuplicates tiles, <= 2 K-steps): cfg2 -1.5 %,
+    // cfg5 -1 %; with 3 K-steps the extra live fragments spill inside the loop (cfg4 2.3x
+    // slower)
+    constexpr bool PREFETCH = XK && PAIRS && KS <= 2 && BICOS_MX_PREFETCH;
     uint32_t m1[T], m2[T], mp[T / 2 > 0 ? T / 2 : 1];
     int b2[T];  // KEYS 2: the base m2[t] is relative to (wave-uniform)
 #pragma unroll
@@ -394,6 +403,39 @@ void search_mx_kernel(SearchArgs a) {
             }
             bprev = B;
         };
+        // XK full blocks with the A fragments of the next block prefetched: `af` holds block
+        // b's fragments on entry; right after the last products that read them are issued,
+        // the ds_reads of block `nb` (if >= 0) go out into the same registers, so their
+        // latency runs under this block's remaining key reductions
+        auto load_af = [&](v4i* af, int b) {
+#pragma unroll
+            for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + 32 * b + j];
+        };
+        auto block_pf = [&](int b, v4i* af, int nb) {
+            const int B = base + 32 * b;
+            v4i an[KS];
+            if constexpr (FREE && PAIRS) {
+#pragma unroll
+                for (int p = 0; p < T / 2; ++p) {
+                    products(0, af, an, cc, cc, 2 * p);
+                    products(1, af, an, cc, cc, 2 * p + 1);
+                    if (p + 1 == T / 2 && nb >= 0) load_af(af, nb);
+                    pair_reduce(p, B, d[0], d[1]);
+                }
+            } else {
+                products(0, af, an, cc, cc, 0);
+                if (T == 1 && nb >= 0) load_af(af, nb);
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    if (t + 1 < T) {
+                        products(t + 1, af, an, cc, cc, t + 1);
+                        if (t + 2 == T && nb >= 0) load_af(af, nb);
+                    }
+                    reduce(t, B, bprev);
+                }
+            }
+            bprev = B;
+        };
         // the block reaching past the image (last chunk): A = 0 there, so D1 = KEY_PAD,
         // D2 = 0 never win. Ascending orders take it last, FREE first.
         auto partial_block = [&](const v16f& cb) {
@@ -446,6 +488,14 @@ void search_mx_kernel(SearchArgs a) {
                         if (++i >= nfull) break;
                     }
                 }
+            } else if constexpr (PREFETCH) {
+                auto bidx = [&](int i) {
+                    int b = sb - i;
+                    return b < 0 ? b + nfull : b;
+                };
+                v4i af[KS];
+                if (nfull > 0) load_af(af, bidx(0));
+                for (int i = 0; i < nfull; ++i) block_pf(bidx(i), af, i + 1 < nfull ? bidx(i + 1) : -1);
             } else
 #endif
             for (int i = 0; i < nfull; ++i) {
@@ -453,6 +503,11 @@ void search_mx_kernel(SearchArgs a) {
                 if (b < 0) b += nfull;
                 block(b, cc, cc);
             }
+        } else if constexpr (XK && PREFETCH) {
+            v4i af[KS];
+            if (nfull > 0) load_af(af, 0);
+            for (int b = 0; b < nfull; ++b) block_pf(b, af, b + 1 < nfull ? b + 1 : -1);
+            if (partial) partial_block(cc);
         } else {
             for (int b = 0; b < nfull; ++b) {
                 if constexpr (!XK) {
