@@ -277,10 +277,24 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     uint32_t* rev_first = fused ? (uint32_t*)(p + map16) : nullptr;
     uint32_t* rev_last = fused && nodupes ? (uint32_t*)(p + map16 + keys) : nullptr;
 
+    // Fused transform -> search (BICOS_FUSE_TRANSFORM=1): the
+    // matrix-core NoDuplicates search computes the LIMITED descriptors from the stacks
+    // itself (no descriptor round trip through HBM, no transform launch). Measured slower
+    // than the two kernels, so opt-in: every search workgroup re-derives the
+    // whole right row it scans.
+    const bool fuse_tf_env = [] {  // read per call (tests toggle it)
+        const char* v = std::getenv("BICOS_FUSE_TRANSFORM");
+        return v && !std::strcmp(v, "1");
+    }();
+    const bool fuse_tf = fuse_tf_env && mx && !consistency && mode == 0 && words <= 4 &&
+                         cols <= 8160;
+
     // 1. descriptor_transform, both stacks in one launch (cpu.cpp:50-59)
-    bicos_hip::TransformArgs ta{s0, s1, d0, d1, n, rows, cols, row_pitch, plane_pitch, dpitch, 0, span};
-    rc = check_hip(bicos_hip::launch_transform(ta, depth, mode, words, st), "transform launch");
-    if (rc) return rc;
+    if (!fuse_tf) {
+        bicos_hip::TransformArgs ta{s0, s1, d0, d1, n, rows, cols, row_pitch, plane_pitch, dpitch, 0, span};
+        rc = check_hip(bicos_hip::launch_transform(ta, depth, mode, words, st), "transform launch");
+        if (rc) return rc;
+    }
 
     // 2. bicos search (cpu.cpp:68-75)
     const bicos_hip::SearchGeometry g = mx ? bicos_hip::SearchGeometry{} : geometry(e, rows, cols, words);
@@ -297,7 +311,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     const bool has_step_ = has_nxcorr && cfg.subpixel_step >= 0;
     const bool fuse_agree = fuse_env && !consistency && has_nxcorr && !has_step_ && !dbl &&
                             (mx ? fuse_env == 2 : g.variant == 16);
-    if (fuse_agree) {
+    if (fuse_agree && !fuse_tf) {
         bicos_hip::SearchArgs sa{d0, d1, nullptr, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
         sa.out_f32 = (float*)disp;
         sa.corr = (float*)corr;
@@ -316,7 +330,19 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
         const bicos_hip::MxGeometry gm = mx_geometry(e, rows, cols, words, used_bits(n, mode));
         if (!consistency) {
             bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
-            rc = check_hip(bicos_hip::launch_search_mx(sa, gm, words, true, st), "search launch");
+            if (fuse_tf) {
+                sa.fused_tf = 1;
+                sa.stack0 = s0;
+                sa.stack1 = s1;
+                sa.n = n;
+                sa.depth = depth;
+                sa.row_pitch = row_pitch;
+                sa.plane_pitch = plane_pitch;
+                sa.stack_bytes = span;
+                sa.tf_magic = (uint32_t)((0x100000000ull + (uint64_t)n - 1) / (uint64_t)n);
+            }
+            rc = check_hip(bicos_hip::launch_search_mx(sa, gm, words, true, st),
+                           fuse_tf ? "fused transform + search launch" : "search launch");
             if (rc) return rc;
         } else {
             // forward and full reverse search (reverse = the same search with the stacks

@@ -20,6 +20,7 @@
 #include "kernels.hpp"
 #include "nxc.hpp"
 #include "stack.hpp"
+#include "transform.hpp"
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -174,100 +175,6 @@ __global__ __launch_bounds__(256) void transform_kernel(TransformArgs a) {
     }
 }
 
-// LIMITED transform, one pixel per lane, the n samples held in registers (MAXN >= n bounds
-// the static arrays; slots t >= n are skipped by wave-uniform branches).
-//
-// Bits are pushed MSB-first into `cur` with v_cmp (-> an SGPR lane mask) + v_addc
-// (cur = 2*cur + bit): 2 full-rate VALU per bit. Each asm block issues all its compares
-// before its adds, so every mask is read >= 2 instructions after it is written (the VALU
-// SGPR-write -> carry-read spacing hipcc itself pads with s_nop 1 on gfx950). Loop bits sit
-// at compile-time positions (t = 0, 1: 3t..3t+2; t >= 2: 6+4(t-2)..9+4(t-2)) because the
-// per-t steps are unrolled by template recursion, so the 32-bit flushes (v_bfrev back to
-// the reference's LSB-first order) are static; only the 4 tail bits and the last partial
-// word land at n-dependent positions.
-//
-// `a < av` (float mean, descriptor_transform.hpp:36-39) is evaluated as `a < ceil(sum/n)`:
-// for integer a, a < RN(sum/n) <=> a*n < sum (the margin 1/n exceeds half an ulp of any
-// value <= 65535) <=> a < ceil(sum/n). ceil(sum/n) = q + (q*n != sum) with
-// q = umulhi(sum, magic), magic = ceil(2^32/n): exact because sum < 2^24 makes the
-// reciprocal's error < 2^-8 < 1/n (n <= 65).
-#define BICOS_CMP(i) "v_cmp_lt_u32_e64 %[m" #i "], %[x" #i "], %[y" #i "]\n\t"
-#define BICOS_ADD(i) "v_addc_co_u32_e64 %[c], %[j], %[c], %[c], %[m" #i "]\n\t"
-#define BICOS_M(i) [m##i] "=&s"(m##i)
-#define BICOS_XY(i) [x##i] "v"(x[i]), [y##i] "v"(y[i])
-
-template <int K>
-__device__ __forceinline__ void push_lt(uint32_t& cur, const uint32_t (&x)[4], const uint32_t (&y)[4]) {
-    uint64_t m0, m1, m2, m3, j;
-    if constexpr (K == 4)
-        asm(BICOS_CMP(0) BICOS_CMP(1) BICOS_CMP(2) BICOS_CMP(3) BICOS_ADD(0) BICOS_ADD(1)
-                BICOS_ADD(2) BICOS_ADD(3)
-            : [c] "+v"(cur), BICOS_M(0), BICOS_M(1), BICOS_M(2), BICOS_M(3), [j] "=&s"(j)
-            : BICOS_XY(0), BICOS_XY(1), BICOS_XY(2), BICOS_XY(3));
-    else if constexpr (K == 3)
-        asm(BICOS_CMP(0) BICOS_CMP(1) BICOS_CMP(2) BICOS_ADD(0) BICOS_ADD(1) BICOS_ADD(2)
-            : [c] "+v"(cur), BICOS_M(0), BICOS_M(1), BICOS_M(2), [j] "=&s"(j)
-            : BICOS_XY(0), BICOS_XY(1), BICOS_XY(2));
-    else if constexpr (K == 2)
-        asm(BICOS_CMP(0) BICOS_CMP(1) "s_nop 0\n\t" BICOS_ADD(0) BICOS_ADD(1)
-            : [c] "+v"(cur), BICOS_M(0), BICOS_M(1), [j] "=&s"(j)
-            : BICOS_XY(0), BICOS_XY(1));
-    else if constexpr (K == 1)
-        asm(BICOS_CMP(0) "s_nop 1\n\t" BICOS_ADD(0)
-            : [c] "+v"(cur), BICOS_M(0), [j] "=&s"(j)
-            : BICOS_XY(0));
-    (void)m0; (void)m1; (void)m2; (void)m3; (void)j;
-}
-#undef BICOS_CMP
-#undef BICOS_ADD
-#undef BICOS_M
-#undef BICOS_XY
-
-// Shift the comparisons x[i] < y[i], i < K, into the descriptor at static bit position POS.
-template <int POS, int K, int WORDS>
-__device__ __forceinline__ void emit_bits(uint32_t& cur, uint32_t (&w)[WORDS], const uint32_t (&x)[4],
-                                          const uint32_t (&y)[4]) {
-    constexpr int room = 32 - POS % 32;
-    if constexpr (K <= room) {
-        push_lt<K>(cur, x, y);
-        if constexpr (K == room) {
-            w[POS / 32] = __builtin_bitreverse32(cur);
-            cur = 0;
-        }
-    } else {
-        push_lt<room>(cur, x, y);
-        w[POS / 32] = __builtin_bitreverse32(cur);
-        cur = 0;
-        uint32_t x2[4] = {0, 0, 0, 0}, y2[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int i = room; i < K; ++i) {
-            x2[i - room] = x[i];
-            y2[i - room] = y[i];
-        }
-        push_lt<K - room>(cur, x2, y2);
-    }
-}
-
-template <int T, int MAXN, int WORDS>
-__device__ __forceinline__ void limited_steps(int n, uint32_t thr, const uint32_t (&v)[MAXN],
-                                              uint32_t& cur, uint32_t (&w)[WORDS]) {
-    if constexpr (T < MAXN - 2) {
-        if (T < n - 2) {
-            constexpr int pos = T < 2 ? 3 * T : 6 + 4 * (T - 2);
-            const uint32_t a = v[T], b = v[T + 1], c = v[T + 2];
-            if constexpr (T < 2) {
-                const uint32_t x[4] = {a, a, a, 0}, y[4] = {b, c, thr, 0};
-                emit_bits<pos, 3, WORDS>(cur, w, x, y);
-            } else {
-                // ps[t-2] < ps[t]  (descriptor_transform.hpp:52-58; ring slot t % 2)
-                const uint32_t x[4] = {a, a, a, v[T - 2] + v[T - 1]}, y[4] = {b, c, thr, a + b};
-                emit_bits<pos, 4, WORDS>(cur, w, x, y);
-            }
-            limited_steps<T + 1, MAXN, WORDS>(n, thr, v, cur, w);
-        }
-    }
-}
-
 template <typename TIn, int WORDS, int MAXN, bool EXACT>
 __global__ __launch_bounds__(256) void transform_limited_kernel(TransformArgs a) {
     const int col = blockIdx.x * 256 + threadIdx.x;
@@ -279,46 +186,8 @@ __global__ __launch_bounds__(256) void transform_limited_kernel(TransformArgs a)
     const uint32_t pp = (uint32_t)a.plane_pitch;
     const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
     // EXACT: n == MAXN, so every `t < n` below is a compile-time constant
-    const int n = EXACT ? MAXN : a.n;
-
-    uint32_t v[MAXN];
-    uint32_t sum = 0;
-#pragma unroll
-    for (int t = 0; t < MAXN; ++t)
-        if (t < n) {
-            v[t] = rd((uint32_t)col, rowoff + (uint32_t)t * pp);
-            sum += v[t];
-        }
-    const uint32_t q = __umulhi(sum, a.magic);
-    const uint32_t thr = q + (q * (uint32_t)n != sum ? 1u : 0u);  // ceil(sum / n)
-
     uint32_t w[WORDS];
-#pragma unroll
-    for (int k = 0; k < WORDS; ++k) w[k] = 0;
-    uint32_t cur = 0;
-    limited_steps<0, MAXN, WORDS>(n, thr, v, cur, w);
-
-    // bits emitted by the loop, the partial word they leave, then the 4 tail bits
-    // (descriptor_transform.hpp:63-68): p[n-2]<p[n-1], p[n-2]<av, p[n-1]<av, ps[n-4]<ps[n-2]
-    const int nl = n >= 4 ? 6 + 4 * (n - 4) : 3 * (n - 2);
-    const int pw = nl >> 5, pm = nl & 31;
-    const uint32_t part = pm ? __builtin_bitreverse32(cur << (32 - pm)) : 0u;
-    // the tail samples sit at n-dependent slots: re-load them (cache hits) rather than
-    // select them out of the register array
-    const uint32_t x = rd((uint32_t)col, rowoff + (uint32_t)(n - 2) * pp);
-    const uint32_t y = rd((uint32_t)col, rowoff + (uint32_t)(n - 1) * pp);
-    const uint32_t pm2 = n >= 4 ? rd((uint32_t)col, rowoff + (uint32_t)(n - 4) * pp) +
-                                      rd((uint32_t)col, rowoff + (uint32_t)(n - 3) * pp)
-                                : 0u;
-    const uint32_t tail = (uint32_t)(x < y) | ((uint32_t)(x < thr) << 1) | ((uint32_t)(y < thr) << 2) |
-                          ((uint32_t)(n < 4 || pm2 < x + y) << 3);
-    const int tw = nl >> 5, toff = nl & 31;
-#pragma unroll
-    for (int k = 0; k < WORDS; ++k) {
-        if (k == pw) w[k] |= part;
-        if (k == tw) w[k] |= tail << toff;
-        if (k == tw + 1 && toff > 28) w[k] |= tail >> (32 - toff);
-    }
+    limited_descriptor<TIn, WORDS, MAXN, EXACT>(rd, (uint32_t)col, rowoff, pp, a.n, a.magic, w);
 
     if (WORDS % 4 == 0) {
 #pragma unroll

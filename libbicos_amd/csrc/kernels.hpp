@@ -47,6 +47,12 @@ struct SearchArgs {
     float threshold = 0.f;
     int has_minvar = 0;
     float minvar = 0.f;             // already scaled by n
+    // fused transform -> search (launch_search_mx; LIMITED, <= 128-bit descriptors, the
+    // NoDuplicates any-order search): desc0/desc1 unused, descriptors computed from
+    // stack0/stack1 (n, depth, row_pitch, plane_pitch above)
+    int fused_tf = 0;
+    uint32_t tf_magic = 0;          // ceil(2^32 / n)
+    uint32_t stack_bytes = 0;       // bytes addressable from each stack base
 };
 
 struct SearchGeometry {

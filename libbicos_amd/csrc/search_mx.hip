@@ -31,6 +31,7 @@
 // (r & 3) + 8 (r >> 2) + 4 (l >> 5) (= col1 in the block) and column l & 31 (= col0).
 #include "kernels.hpp"
 #include "nxc.hpp"
+#include "transform.hpp"
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -170,9 +171,20 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 // blocks still do it). The result is exact whatever the data: the order only changes speed.
 // Keys stay relative to the base B of the block being reduced (shifts by the signed
 // B - B_prev); C = 768 + (8160 + col1 % 32) * 2^-14 keeps both fields in [0, 16383].
-template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, int FUSE = 0>
+// TF: 0 = descriptors from desc0 / desc1; 1 / 2 = fused transform -> search on u8 / u16
+// stacks (LIMITED): the left descriptors of the wave's tiles and the right row's, chunk by
+// chunk, are computed from the stacks (transform.hpp) instead of read from HBM
+template <int TIn_bytes>
+struct tf_type { using type = uint8_t; };
+template <>
+struct tf_type<2> { using type = uint16_t; };
+constexpr int tf_maxn(int words) { return words == 1 ? 9 : words == 2 ? 17 : 33; }
+
+template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, int FUSE = 0, int TF = 0>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void search_mx_kernel(SearchArgs a) {
+    static_assert(TF == 0 || WORDS <= 4, "fused transform: descriptors up to 128 bits");
+    using TTF = typename tf_type<TF == 2 ? 2 : 1>::type;
     constexpr bool XK = KEYS != 0;
     constexpr bool FREE = KEYS == 2;
     static_assert(!FREE || NODUPES, "KEYS 2 is the NoDuplicates search");
@@ -213,11 +225,27 @@ void search_mx_kernel(SearchArgs a) {
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const int c0 = c0_wave + 32 * t + j;
+        uint32_t wl[WORDS];  // TF: the pixel's descriptor, computed from the left stack
+        if constexpr (TF != 0) {
+#pragma unroll
+            for (int q = 0; q < WORDS; ++q) wl[q] = 0;
+            if (c0 < cols)
+                limited_descriptor<TTF, WORDS, tf_maxn(WORDS), false>(
+                    StackReader<TTF>(a.stack0, a.stack_bytes), (uint32_t)c0,
+                    (uint32_t)row * (uint32_t)a.row_pitch, (uint32_t)a.plane_pitch, a.n, a.tf_magic, wl);
+        }
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const int w = 2 * s + h;
             uint32_t x = 0;
-            if (c0 < cols && w < WORDS) x = row0[(size_t)c0 * WORDS + w];
+            if constexpr (TF != 0) {
+                // word 2s + h: a select of the two static slots (no dynamic register index)
+                const uint32_t lo = 2 * s < WORDS ? wl[(2 * s) % WORDS] : 0u;
+                const uint32_t hi = 2 * s + 1 < WORDS ? wl[(2 * s + 1) % WORDS] : 0u;
+                x = h ? hi : lo;
+            } else {
+                if (c0 < cols && w < WORDS) x = row0[(size_t)c0 * WORDS + w];
+            }
             if (WORDS == 8 && KS == 4 && w == 7) x &= 0x7FFFFFFFu;  // bit 255 masked (see below)
             bf[t][s] = expand_bits(x, LUT_B);
         }
@@ -350,10 +378,23 @@ void search_mx_kernel(SearchArgs a) {
         // expand the chunk's right descriptors: one col1 per thread, all its words
         for (int c = threadIdx.x; expand && c < chunk; c += blockDim.x) {
             const int c1 = base + c;
+            uint32_t wr[WORDS];  // TF: the right pixel's descriptor from the right stack
+            if constexpr (TF != 0) {
+#pragma unroll
+                for (int q = 0; q < WORDS; ++q) wr[q] = 0;
+                if (c1 < cols)
+                    limited_descriptor<TTF, WORDS, tf_maxn(WORDS), false>(
+                        StackReader<TTF>(a.stack1, a.stack_bytes), (uint32_t)c1,
+                        (uint32_t)row * (uint32_t)a.row_pitch, (uint32_t)a.plane_pitch, a.n, a.tf_magic, wr);
+            }
 #pragma unroll
             for (int w = 0; w < WL; ++w) {
                 uint32_t x = 0;
-                if (c1 < cols && w < WORDS) x = row1[(size_t)c1 * WORDS + w];
+                if constexpr (TF != 0) {
+                    x = w < WORDS ? wr[w % WORDS] : 0u;
+                } else {
+                    if (c1 < cols && w < WORDS) x = row1[(size_t)c1 * WORDS + w];
+                }
                 if (WORDS == 8 && KS == 4 && w == 7) x &= 0x7FFFFFFFu;
                 lds_mx[w * chunk + c] = expand_bits(x, LUT_A);
             }
@@ -610,8 +651,16 @@ hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
             if (a.out_f32) return a.depth == 2 ? search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 2>
                                                : search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 1>;
         }
+        if constexpr (KEYS == 2 && WORDS <= 4) {
+            if (a.fused_tf) return a.depth == 2 ? search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 0, 2>
+                                                : search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 0, 1>;
+        }
         return search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 0>;
     };
+    // the fused transform: the NoDuplicates any-order search (KEYS 2), up to 128 bits,
+    // u8 / u16 stacks, not with the fused agree
+    if (a.fused_tf && (KEYS != 2 || WORDS > 4 || a.out_f32 || (a.depth != 1 && a.depth != 2)))
+        return hipErrorInvalidValue;
     if (a.out_f32 && (!NODUPES || (a.depth != 1 && a.depth != 2))) return hipErrorInvalidValue;
     const auto kern = pick();
     if (lds > 64 * 1024) {

@@ -371,6 +371,30 @@ def test_fused_search_agree_equals_separate(gpu, n, H, W, dt, minvar):
         same(host(fc), host(sc))
 
 
+# The fused transform -> search (BICOS_FUSE_TRANSFORM=1: descriptors computed from the
+# stacks inside the matrix-core search) == the transform kernel +
+# search, byte for byte, for every descriptor width it covers (LIMITED, <= 128 bits), u8 /
+# u16, ragged widths, NXC / subpixel / no NXC; and the oracle on one case.
+@pytest.mark.parametrize("n,H,W,dt,kw", [
+    (2, 3, 40, np.uint8, {}), (8, 5, 700, np.uint8, dict(nxcorr_threshold=0.8)),
+    (9, 4, 333, np.uint16, dict(nxcorr_threshold=0.5, min_variance=1.0)),
+    (17, 4, 1300, np.uint16, dict(nxcorr_threshold=0.8)), (24, 3, 97, np.uint8, {}),
+    (33, 6, 2048, np.uint8, dict(nxcorr_threshold=0.96)),
+    (33, 4, 1030, np.uint8, dict(nxcorr_threshold=0.9, subpixel_step=0.25))])
+def test_fused_transform_search_equals_separate(gpu, oracle, n, H, W, dt, kw, monkeypatch):
+    L, R = stereo_stack(n, H, W, dt, dmin=3, drange=30, seed=n * 7 + W)
+    monkeypatch.setenv("BICOS_FUSE_TRANSFORM", "0")
+    d_ref, c_ref = gpu_match(gpu, L, R, **kw)
+    monkeypatch.setenv("BICOS_FUSE_TRANSFORM", "1")
+    d_f, c_f = gpu_match(gpu, L, R, **kw)
+    same(d_f, d_ref)
+    if c_ref is not None:
+        same(c_f, c_ref)
+    if n == 33 and W == 2048:
+        do, _ = oracle.match(L, R, cfg_of(oracle, **kw))
+        same(d_f, do)
+
+
 def test_errors(gpu):
     import torch
     from libbicos_amd import BicosError
