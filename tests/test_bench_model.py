@@ -1,0 +1,58 @@
+"""The work models bench.py reports its rooflines with (CPU only): x-step counts of the
+subpixel loop, K-steps and FLOPs of the matrix-core search, the issue-rate bounds."""
+import numpy as np
+import pytest
+
+import bench
+
+
+def _ref_steps(step):
+    # the reference's loop, accumulated in float32 (agree.hpp:122)
+    x, k = np.float32(-1.0), 0
+    while x <= np.float32(1.0):
+        k += 1
+        x = np.float32(x + np.float32(step))
+    return k
+
+
+@pytest.mark.parametrize("step", [0.1, 0.25, 0.5, 0.05, 0.7, 2.0, 1.0 / 3.0])
+def test_subpixel_steps_follow_the_float_loop(step):
+    assert bench.subpixel_steps(step) == _ref_steps(step)
+
+
+def test_subpixel_steps_known_values():
+    assert bench.subpixel_steps(0.1) == 20   # 1.0000001 > 1 after 20 additions
+    assert bench.subpixel_steps(0.5) == 5
+    assert bench.subpixel_steps(2.0) == 2
+
+
+@pytest.mark.parametrize("words,bits,ks", [(1, 25, 1), (2, 61, 1), (4, 125, 2), (8, 154, 3),
+                                           (8, 192, 3), (8, 193, 4), (8, 0, 4), (4, 0, 2)])
+def test_mx_ksteps(words, bits, ks):
+    assert bench.mx_ksteps(words, bits) == ks
+
+
+def test_mx_flops_cfg2_and_cfg4():
+    cfg2 = bench.CONFIGS["cfg2"]
+    alg, exe = bench.mx_flops(1536, 2048, 4, cfg2["cfg"], 4 * 33 - 5)
+    assert alg == exe == 1536 * 2048 * 2048 * 2 * 128
+    cfg4 = bench.CONFIGS["cfg4"]
+    alg, exe = bench.mx_flops(1536, 2048, 8, cfg4["cfg"], 4 * 40 - 5)
+    pairs = 2 * 1536 * 2048 * 2048  # forward + reverse
+    assert alg == pairs * 2 * 256 and exe == pairs * 2 * 192
+
+
+def test_configs_match_the_baseline():
+    c = bench.CONFIGS
+    assert (c["cfg2"]["n"], c["cfg2"]["H"], c["cfg2"]["W"]) == (33, 1536, 2048)
+    assert c["cfg3"]["cfg"]["subpixel_step"] == 0.1 and c["cfg3"]["cfg"]["min_variance"] == 2.0
+    assert c["cfg4"]["n"] >= 40 and c["cfg4"]["cfg"]["variant"] == 1
+    assert (c["cfg5"]["H"], c["cfg5"]["W"]) == (2160, 3840)
+    assert (c["cfg1"]["n"], c["cfg1"]["H"], c["cfg1"]["W"]) == (8, 480, 640)
+
+
+def test_key_pair_bound_is_positive_and_ordered():
+    # duplicate detection costs issue slots: the NoDuplicates bound is the lower one
+    nd = bench.mx_key_pair_peak(4, {"variant": 0})
+    cons = bench.mx_key_pair_peak(8, {"variant": 1, "no_dupes": False})
+    assert 0 < nd < cons
