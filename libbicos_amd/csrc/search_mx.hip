@@ -162,9 +162,10 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 //
 // KEYS 2. NoDuplicates needs the LAST column at the minimum cost only to compare it with
 // the first; a block none of whose keys reaches the running minimum cost cannot hold it. So
-// the running first minimum is shared by the two lane halves every block (v_permlane32_swap
-// + one v_min3), each half tests its own block minimum against it (<= in cost), and the
-// xor + min tree of the last minimum runs only when some lane of the wave passes. Blocks
+// each tile's block minimum is combined over the two lane halves (tiles in pairs: one
+// v_permlane32_swap of two tiles' minima, see pair_reduce) and tested against the tile's
+// running first minimum (<= in cost), and the xor + min tree of the last minimum runs only
+// for a tile some lane of which passes (one wave-uniform branch per pair). Blocks
 // are visited from the wave's own col0 downwards (chunks from the workgroup's, wrapping):
 // a stereo match lies at col1 <= col0 within a few blocks, the running minimum reaches it
 // early, and the rest of the row skips that half of the VALU work (cfg2 synthetic: ~6 % of
