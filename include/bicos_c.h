@@ -155,6 +155,35 @@ int bicos_match_host(bicos_engine* e, const void* const* stack0, const void* con
                      int rows, int cols, size_t step, int depth, const BicosConfig* cfg,
                      int has_nxcorr, void* disparity, void* corrmap);
 
+/* ------------------------------------------------ single-process multi-GPU */
+/* One frame matched on several GPUs from one process (the reference has
+ * no multi-GPU API -- these extend bicos_match_host / bicos_match_device, whose conventions
+ * they keep). The frame's rows are split into contiguous bands, band b on devices[b] with
+ * that device's default engine. Every stage of the match is row-local, so the maps are
+ * byte-identical to the one-GPU call. devices may repeat (bands on one GPU then run one
+ * after another on its engine). Both calls are synchronous. */
+
+/* Host buffers, bicos_match_host's arguments: the rows are split into min(ndev, rows)
+ * bands whose heights differ by at most one (the first rows % ndev bands get the extra
+ * row); one host thread per band runs the banded upload -> match -> download pipeline of
+ * its GPU over that GPU's own PCIe link and writes its rows of the maps straight into
+ * `disparity` / `corrmap`. */
+int bicos_match_host_multi(const int* devices, int ndev, const void* const* stack0,
+                           const void* const* stack1, int n, int rows, int cols, size_t step,
+                           int depth, const BicosConfig* cfg, int has_nxcorr, void* disparity,
+                           void* corrmap);
+
+/* Device-resident bands: band b (band_rows[b] rows, in frame order) lives on devices[b] as
+ * planar stacks stack0[b] / stack1[b] with row_pitch[b] / plane_pitch[b] (elements, as in
+ * bicos_match_device). Each GPU matches its band; the maps are gathered into `disparity` /
+ * `corrmap` on devices[0] (dense, sum(band_rows) x cols; corrmap may be NULL) by peer
+ * copies over xGMI -- band 0 is written in place. */
+int bicos_match_bands_device(const int* devices, int ndev, const void* const* stack0,
+                             const void* const* stack1, const int* band_rows,
+                             const size_t* row_pitch, const size_t* plane_pitch, int n, int cols,
+                             int depth, const BicosConfig* cfg, int has_nxcorr, void* disparity,
+                             void* corrmap);
+
 /* Stage entry points (tests, benchmarks, custom pipelines). Same conventions.
  * desc buffers: rows x desc_pitch uint32 with desc_pitch = bicos_desc_pitch(cols, words). */
 size_t bicos_desc_pitch(int cols, int words);

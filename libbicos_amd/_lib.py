@@ -56,7 +56,8 @@ EXPORTS = (
     "BICOS_CreateDefaultConfig", "BICOS_FreeConfig", "BICOS_FreeResult", "BICOS_Match",
     "BICOS_InvalidDisparityFloat", "BICOS_InvalidDisparityInt16", "bicos_last_error",
     "bicos_engine_create", "bicos_engine_default", "bicos_engine_destroy", "bicos_engine_tune", "bicos_descriptor_words", "bicos_output_type",
-    "bicos_match_device", "bicos_match_host", "bicos_desc_pitch", "bicos_transform_device", "bicos_search_device",
+    "bicos_match_device", "bicos_match_host", "bicos_match_host_multi", "bicos_match_bands_device",
+    "bicos_desc_pitch", "bicos_transform_device", "bicos_search_device",
     "bicos_agree_device", "bicos_subpixel_device", "bicos_search_agree_device", "bicos_build_info",
 )
 
@@ -121,6 +122,13 @@ def lib() -> ctypes.CDLL:
     L.bicos_match_device.restype = I
     L.bicos_match_host.argtypes = [P, PP, PP, I, I, I, Z, I, ctypes.POINTER(BicosConfig), I, P, P]
     L.bicos_match_host.restype = I
+    PZ = ctypes.POINTER(ctypes.c_size_t)
+    L.bicos_match_host_multi.argtypes = [PI, I, PP, PP, I, I, I, Z, I,
+                                         ctypes.POINTER(BicosConfig), I, P, P]
+    L.bicos_match_host_multi.restype = I
+    L.bicos_match_bands_device.argtypes = [PI, I, PP, PP, PI, PZ, PZ, I, I, I,
+                                           ctypes.POINTER(BicosConfig), I, P, P]
+    L.bicos_match_bands_device.restype = I
     L.bicos_desc_pitch.argtypes = [I, I]
     L.bicos_desc_pitch.restype = Z
     L.bicos_transform_device.argtypes = [P, I, I, I, Z, Z, I, I, I, P, P]

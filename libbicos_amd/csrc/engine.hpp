@@ -77,6 +77,7 @@ struct Status {
 
 void set_error(int code, const std::string& msg);
 int fail(int code, const std::string& msg);
+const char* last_error();  // this thread's last message
 int check_hip(hipError_t e, const char* what);
 
 // Reserve `bytes` of engine workspace (device), stream-ordered on `st`: a buffer that

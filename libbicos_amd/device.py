@@ -12,7 +12,7 @@ from __future__ import annotations
 
 import ctypes
 import dataclasses
-from typing import Optional, Tuple
+from typing import Optional, Sequence, Tuple
 
 import torch
 
@@ -257,6 +257,51 @@ def default_engine(device=None) -> Engine:
     if idx not in _ENGINES:
         _ENGINES[idx] = Engine(idx, shared=True)
     return _ENGINES[idx]
+
+
+def match_bands(bands0: Sequence[torch.Tensor], bands1: Sequence[torch.Tensor],
+                cfg: Optional[MatchConfig] = None, want_corrmap: bool = True
+                ) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+    """Single-process multi-GPU match (bicos_match_bands_device):
+    bands0[b] / bands1[b] are the planar stacks [n, rows_b, cols] of row band b (bands in
+    frame order), each on the GPU that matches it. Returns the whole frame's (disparity,
+    corrmap) on bands0[0]'s device, gathered there by peer copies. Synchronous: the work
+    queued on every band device's current stream is finished first."""
+    cfg = cfg or MatchConfig()
+    if len(bands0) == 0 or len(bands0) != len(bands1):
+        raise ValueError("need the same number (>= 1) of left and right bands")
+    k = len(bands0)
+    shapes = [_check_stack(t) for t in bands0]
+    n, _, cols, _, _ = shapes[0]
+    for b in range(k):
+        t0, t1 = bands0[b], bands1[b]
+        if t0.shape[0] != n or t0.shape[2] != cols or t0.dtype != bands0[0].dtype:
+            raise ValueError("every band needs the same n, cols and dtype")
+        if tuple(t1.shape) != tuple(t0.shape) or t1.stride() != t0.stride() or \
+                t1.dtype != t0.dtype or t1.device != t0.device:
+            raise ValueError("bands1[%d] must match bands0[%d] in shape, strides, dtype, device"
+                             % (b, b))
+    c, has_nxcorr = cfg.to_c()
+    root = bands0[0].device
+    rows = sum(int(t.shape[1]) for t in bands0)
+    disp_dtype = torch.float32 if has_nxcorr else torch.int16
+    corr_dtype = torch.float64 if cfg.precision else torch.float32
+    out = torch.empty((rows, cols), dtype=disp_dtype, device=root)
+    corrmap = torch.empty((rows, cols), dtype=corr_dtype, device=root) \
+        if has_nxcorr and want_corrmap else None
+    for dev in {t.device for t in bands0} | {root}:
+        torch.cuda.synchronize(dev)
+    devs = (ctypes.c_int * k)(*[t.device.index or 0 for t in bands0])
+    p0 = (ctypes.c_void_p * k)(*[t.data_ptr() for t in bands0])
+    p1 = (ctypes.c_void_p * k)(*[t.data_ptr() for t in bands1])
+    br = (ctypes.c_int * k)(*[int(t.shape[1]) for t in bands0])
+    rp = (ctypes.c_size_t * k)(*[s[3] for s in shapes])
+    pp = (ctypes.c_size_t * k)(*[s[4] for s in shapes])
+    rc = _lib.lib().bicos_match_bands_device(
+        devs, k, p0, p1, br, rp, pp, n, cols, _depth(bands0[0]), ctypes.byref(c), has_nxcorr,
+        out.data_ptr(), corrmap.data_ptr() if corrmap is not None else None)
+    _lib.check(rc, "bicos_match_bands_device")
+    return out, corrmap
 
 
 def match(stack0: torch.Tensor, stack1: torch.Tensor, cfg: Optional[MatchConfig] = None,

@@ -170,8 +170,12 @@ def _marshal(stack):
     return data, rows, cols, types, keep
 
 
-def match(stack0, stack1, cfg=None):
+def match(stack0, stack1, cfg=None, devices=None):
     """reference pybicos/__init__.py:199-244 -> (disparity, corrmap).
+
+    devices (an extension; the reference is single-GPU): a sequence of GPU indices to split
+    the frame's rows over from this process (bicos_match_host_multi: one band per device,
+    each uploaded over its own GPU's link); the maps are byte-identical to the one-GPU call.
 
     Same inputs, outputs, dtypes and errors as the reference wrapper (which goes through
     BICOS_Match: NXC always on, so float32 disparity; corrmap float32, or float64 with
@@ -194,8 +198,16 @@ def match(stack0, stack1, cfg=None):
     cdtype = np.float64 if cfg._c_config.contents.precision else np.float32
     disparity = np.empty((rows, cols), ddtype)
     corrmap = np.empty((rows, cols), cdtype)
-    rc = L.bicos_match_host(None, d0, d1, len(k0), rows, cols, 0, f.dtype.itemsize,
-                            cfg._c_config, 1, disparity.ctypes.data, corrmap.ctypes.data)
+    if devices is None:
+        rc = L.bicos_match_host(None, d0, d1, len(k0), rows, cols, 0, f.dtype.itemsize,
+                                cfg._c_config, 1, disparity.ctypes.data, corrmap.ctypes.data)
+    else:
+        devs = [int(d) for d in devices]
+        if not devs:
+            raise ValueError("devices must name at least one GPU")
+        rc = L.bicos_match_host_multi((ctypes.c_int * len(devs))(*devs), len(devs), d0, d1,
+                                      len(k0), rows, cols, 0, f.dtype.itemsize, cfg._c_config, 1,
+                                      disparity.ctypes.data, corrmap.ctypes.data)
     del k0, k1
     if rc != 0:
         raise RuntimeError("BICOS matching failed: " + L.bicos_last_error().decode(errors="replace"))

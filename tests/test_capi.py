@@ -136,3 +136,26 @@ def test_device_out_validation_rejects_bad_tensors():
                    (torch.float32,), cpu)
     with pytest.raises(ValueError, match="must be on"):
         _check_out(good, "out", (4, 6), (torch.float32,), torch.device("meta"))
+
+
+def test_multi_gpu_entries_validate_before_any_gpu_call(blib):
+    """bicos_match_host_multi / bicos_match_bands_device reject bad arguments (no device
+    list, n < 2, bad depth, negative band heights) before touching a GPU."""
+    from libbicos_amd._lib import BicosConfig
+    cfg = blib.BICOS_CreateDefaultConfig()
+    PP = ctypes.c_void_p * 4
+    imgs = PP()
+    one = (ctypes.c_int * 1)(0)
+    rc = blib.bicos_match_host_multi(None, 0, imgs, imgs, 4, 8, 8, 0, 1, cfg, 1, None, None)
+    assert rc == -1 and b"device" in blib.bicos_last_error()
+    rc = blib.bicos_match_host_multi(one, 1, imgs, imgs, 1, 8, 8, 0, 1, cfg, 1, None, None)
+    assert rc == -1 and b"two images" in blib.bicos_last_error()
+    rc = blib.bicos_match_host_multi(one, 1, imgs, imgs, 4, 8, 8, 0, 3, cfg, 1, None, None)
+    assert rc == -1 and b"depth" in blib.bicos_last_error()
+    br = (ctypes.c_int * 1)(8)
+    pz = (ctypes.c_size_t * 1)(8)
+    rc = blib.bicos_match_bands_device(None, 0, imgs, imgs, br, pz, pz, 4, 8, 1, cfg, 1, None, None)
+    assert rc == -1 and b"device" in blib.bicos_last_error()
+    rc = blib.bicos_match_bands_device(one, 1, imgs, imgs, None, pz, pz, 4, 8, 1, cfg, 1, None, None)
+    assert rc == -1 and b"band" in blib.bicos_last_error()
+    blib.BICOS_FreeConfig(cfg)
