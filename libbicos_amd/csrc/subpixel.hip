@@ -6,9 +6,29 @@
 // SIMD, arrays past 256 registers) run the SLP build: subpixel_wide.hip.
 #include "subpixel.hpp"
 
+#include <cstdlib>
+
 namespace bicos_hip {
 
 namespace {
+
+// n = 25..33 runs the LDS-staged kernel (subpixel.hpp, NCS) at 3 waves/SIMD instead of the
+// register-only one at 2 (213 VGPRs): 0.638 vs 0.676 ms at n = 33 (A/B in one session).
+// BICOS_SP33_NCS = the C slots held in LDS with every D0 slot: the fewest that fit 168 VGPRs
+// without spills (16: 128 B/lane of scratch); 18 slots + 33 = 51 KiB per 256-thread
+// workgroup, 3 per CU. The same staging for n = 17..24 at 4 waves/SIMD (12 C slots, 36 KiB)
+// measured 2 % slower than its register-only kernel at 3 waves (0.449 vs 0.441 ms): not used.
+#ifndef BICOS_SP33_NCS
+#define BICOS_SP33_NCS 18
+#endif
+// BICOS_SUBPIXEL_STAGE=0: the register-only kernel (A/B)
+bool subpixel_stage() {
+    static const bool on = [] {
+        const char* v = std::getenv("BICOS_SUBPIXEL_STAGE");
+        return !(v && v[0] == '0');
+    }();
+    return on;
+}
 
 template <typename TIn, typename TPrec>
 hipError_t launch_subpixel_t(const AgreeArgs& a, int depth, bool dbl, hipStream_t st) {
@@ -16,7 +36,12 @@ hipError_t launch_subpixel_t(const AgreeArgs& a, int depth, bool dbl, hipStream_
     if (n <= 8) return launch_subpixel_m<TIn, TPrec, 8, 2>(a, st);
     if (n <= 16) return launch_subpixel_m<TIn, TPrec, 16, 9>(a, st);
     if (n <= 24) return launch_subpixel_m<TIn, TPrec, 24, 17>(a, st);
-    if (n <= 33) return launch_subpixel_m<TIn, TPrec, 33, 25>(a, st);
+    if (n <= 33) {
+        if constexpr (sizeof(TPrec) == 4) {
+            if (subpixel_stage()) return launch_subpixel_m<TIn, TPrec, 33, 25, BICOS_SP33_NCS, 3>(a, st);
+        }
+        return launch_subpixel_m<TIn, TPrec, 33, 25>(a, st);
+    }
     if (n <= 40) return launch_subpixel_m<TIn, TPrec, 40, 34>(a, st);
     return launch_subpixel_wide(a, depth, dbl, st);
 }

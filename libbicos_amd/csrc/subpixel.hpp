@@ -59,8 +59,20 @@ __device__ __forceinline__ float interp_wrapped(float A, float B, float C, float
 // every chain op has independent interpolation work beside it and the register footprint
 // is that of one step. nsteps is the host's count of x = -1, -1+step, ... <= 1, accumulated
 // in float exactly as the reference's loop (engine.cpp subpixel_steps).
-template <typename TIn, typename TPrec, int MAXN, int LO>
-__global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
+// NCS >= 0 (float, MAXN <= 40): the centred left samples D0 of every slot and the C of the
+// top NCS slots live in LDS instead of registers ([slot][thread], one conflict-free
+// ds_read_b32 with an immediate offset per use; each thread reads only what it wrote, so no
+// barrier), which brings the kernel under WPE waves/SIMD's register budget. The arithmetic
+// is unchanged.
+template <typename TIn, typename TPrec, int MAXN, int LO, int NCS = -1, int WPE = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+void subpixel_kernel(AgreeArgs a) {
+    constexpr bool STG = NCS >= 0;
+    static_assert(!STG || (sizeof(TPrec) == 4 && MAXN <= 40 && NCS <= MAXN), "LDS staging: float, n <= 40");
+    constexpr int CS = MAXN - (NCS > 0 ? NCS : 0);  // first C slot held in LDS
+    __shared__ float sD0[STG ? MAXN : 1][256];
+    __shared__ float sC[STG && NCS > 0 ? NCS : 1][256];
+    const int tid = threadIdx.x;
     int tile, row;
     xcd_rows(tile, row);
     const int col = tile * 256 + threadIdx.x;
@@ -85,7 +97,7 @@ __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
             // left: mean, centred samples and variance are the same for every x
             // padded slots re-read plane 0 (in bounds) and are zeroed; int -> float via
             // small_int_to_float (two full-rate ops instead of a quarter-rate v_cvt_f32_*)
-            TPrec D0[MAXN];
+            TPrec D0[STG ? 1 : MAXN];
             float A[MAXN], B[MAXN], C[MAXN];
             uint32_t s = 0;
 #pragma unroll
@@ -101,18 +113,49 @@ __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
                 A[t] = live ? 0.5f * small_int_to_float(y0 - 2 * y1 + y2) : 0.f;
                 B[t] = live ? 0.5f * small_int_to_float(y2 - y0) : 0.f;
                 C[t] = live ? small_int_to_float(y1) : 0.f;
-                D0[t] = live ? (TPrec)small_int_to_float((int)l) : (TPrec)0;
+                const TPrec lf = live ? (TPrec)small_int_to_float((int)l) : (TPrec)0;
+                if constexpr (STG) {
+                    sD0[t][tid] = lf;  // the raw sample; centred below
+                    if (t >= CS) sC[t >= CS ? t - CS : 0][tid] = C[t];
+                    // at most 8 slots' loads in flight: the prologue stays inside the
+                    // 168-register budget of 3 waves/SIMD too
+                    if (t % 8 == 7) asm volatile("" ::: "memory");
+                } else {
+                    D0[t] = lf;
+                }
                 s += live ? l : 0u;
             }
+            // The empty asm statements with a memory clobber (here, and at the top of every x
+            // step) stop the compiler from forwarding stored values or hoisting the
+            // loop-invariant LDS reads, either of which would keep the arrays in registers.
+            if constexpr (STG) asm volatile("" ::: "memory");
             const TPrec m0 = div_p((TPrec)s, (TPrec)n);
             TPrec v0 = 0;
 #pragma unroll
             for (int t = 0; t < MAXN; ++t) {
                 const bool live = t < LO || t < n;
-                D0[t] = live ? D0[t] - m0 : (TPrec)0;
-                v0 = fma_p(D0[t], D0[t], v0);
+                if constexpr (STG) {
+                    const TPrec dc = live ? sD0[t][tid] - m0 : (TPrec)0;
+                    sD0[t][tid] = dc;
+                    v0 = fma_p(dc, dc, v0);
+                } else {
+                    D0[t] = live ? D0[t] - m0 : (TPrec)0;
+                    v0 = fma_p(D0[t], D0[t], v0);
+                }
             }
+            if constexpr (STG) asm volatile("" ::: "memory");
             const bool v0_low = a.has_minvar && v0 < minvar;
+            // the left sample / C of slot t: registers, or this thread's LDS slot
+            auto d0_of = [&](int t) -> TPrec {
+                if constexpr (STG) return sD0[t][tid];
+                else return D0[t];
+            };
+            auto c_of = [&](int t) -> float {
+                if constexpr (STG) {
+                    if (t >= CS) return sC[t >= CS ? t - CS : 0][tid];
+                }
+                return C[t];
+            };
 
             float best_x = 0.f;
             TPrec best = -1;
@@ -137,10 +180,11 @@ __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
                 // in-order fma chains) and interpolates step k+1 into the same registers.
 #pragma unroll
                 for (int t = 0; t < MAXN; ++t) {
-                    IV[t] = interp_wrapped<TIn>(A[t], B[t], C[t], x);
+                    IV[t] = interp_wrapped<TIn>(A[t], B[t], c_of(t), x);
                     sf[t & 3] += IV[t];
                 }
                 for (int k = 0; k < a.nsteps; ++k) {
+                    if constexpr (STG) asm volatile("" ::: "memory");
                     const TPrec m1 = div_p((TPrec)((sf[0] + sf[1]) + (sf[2] + sf[3])), (TPrec)n);
                     const float xn = x + step;
                     TPrec cov = 0, v1 = 0;
@@ -151,9 +195,9 @@ __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
                         for (int t = 0; t < MAXN; ++t) {
                             TPrec x1 = (TPrec)IV[t] - m1;
                             if (t >= LO) x1 = t < n ? x1 : (TPrec)0;
-                            cov = fma_p(D0[t], x1, cov);
+                            cov = fma_p(d0_of(t), x1, cov);
                             v1 = fma_p(x1, x1, v1);
-                            IV[t] = interp_wrapped<TIn>(A[t], B[t], C[t], xn);
+                            IV[t] = interp_wrapped<TIn>(A[t], B[t], c_of(t), xn);
                         }
                         sf[0] = sf[1] = sf[2] = sf[3] = 0.f;
 #pragma unroll
@@ -163,7 +207,7 @@ __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
                         for (int t = 0; t < MAXN; ++t) {
                             TPrec x1 = (TPrec)IV[t] - m1;
                             if (t >= LO) x1 = t < n ? x1 : (TPrec)0;
-                            cov = fma_p(D0[t], x1, cov);
+                            cov = fma_p(d0_of(t), x1, cov);
                             v1 = fma_p(x1, x1, v1);
                         }
                     }
@@ -201,13 +245,13 @@ __global__ __launch_bounds__(256) void subpixel_kernel(AgreeArgs a) {
     if (a.corrmap) ((TPrec*)a.corrmap)[o] = corr;
 }
 
-template <typename TIn, typename TPrec, int MAXN, int LO>
+template <typename TIn, typename TPrec, int MAXN, int LO, int NCS = -1, int WPE = 1>
 hipError_t launch_subpixel_m(const AgreeArgs& a, hipStream_t st) {
     dim3 grid((a.cols + 255) / 256, a.rows);
     if (a.n == MAXN)
-        hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN, MAXN>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN, MAXN, NCS, WPE>), grid, dim3(256), 0, st, a);
     else
-        hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN, LO>), grid, dim3(256), 0, st, a);
+        hipLaunchKernelGGL((subpixel_kernel<TIn, TPrec, MAXN, LO, NCS, WPE>), grid, dim3(256), 0, st, a);
     return hipGetLastError();
 }
 
