@@ -130,6 +130,7 @@ void subpixel_kernel(AgreeArgs a) {
             // loop-invariant LDS reads, either of which would keep the arrays in registers.
             if constexpr (STG) asm volatile("" ::: "memory");
             const TPrec m0 = div_p((TPrec)s, (TPrec)n);
+            const float rn = div_p(1.f, (float)n);  // RN(1/n) for nxc::div_by_n
             TPrec v0 = 0;
 #pragma unroll
             for (int t = 0; t < MAXN; ++t) {
@@ -185,7 +186,12 @@ void subpixel_kernel(AgreeArgs a) {
                 }
                 for (int k = 0; k < a.nsteps; ++k) {
                     if constexpr (STG) asm volatile("" ::: "memory");
-                    const TPrec m1 = div_p((TPrec)((sf[0] + sf[1]) + (sf[2] + sf[3])), (TPrec)n);
+                    const float sum = (sf[0] + sf[1]) + (sf[2] + sf[3]);
+                    TPrec m1;
+                    if constexpr (sizeof(TPrec) == 4)
+                        m1 = nxc::div_by_n(sum, (float)n, rn);
+                    else
+                        m1 = div_p((TPrec)sum, (TPrec)n);
                     const float xn = x + step;
                     TPrec cov = 0, v1 = 0;
                     // two copies of the body: a wave-uniform test inside the unrolled t loop
