@@ -42,6 +42,20 @@ __device__ __forceinline__ float sqrt_p(float x) {
     return (xs == 0.f || xs == __builtin_inff() || !(xs > 0.f)) ? __builtin_amdgcn_sqrtf(x) : s;
 }
 __device__ __forceinline__ double sqrt_p(double a) { return __dsqrt_rn(a); }
+// sqrt_p for x = 0 or 2^-96 <= x < +inf only -- the product of two variances of integer
+// samples (each 0 or >= (1/65)^2, see subpixel.hpp) -- without the tiny-input scaling and the
+// special-value select: x = 0 gives s = 0 (r_dn is NaN, r_up is 0: neither fix-up fires)
+__device__ __forceinline__ float sqrt_p_var(float x) {
+    float s = __builtin_amdgcn_sqrtf(x);
+    const int si = __float_as_int(s);
+    const float s_dn = __int_as_float(si - 1);
+    const float s_up = __int_as_float(si + 1);
+    const float r_dn = __builtin_fmaf(-s_dn, s, x);
+    const float r_up = __builtin_fmaf(-s_up, s, x);
+    s = r_dn <= 0.f ? s_dn : s;
+    return r_up > 0.f ? s_up : s;
+}
+__device__ __forceinline__ double sqrt_p_var(double a) { return __dsqrt_rn(a); }
 
 // s / n correctly rounded for an integer-valued s in [0, 65535 n] and 2 <= n <= 65, given
 // rn = RN(1 / n): q0 = RN(s rn), r = s - q0 n (exact by fma), RN(q0 + r rn). Checked

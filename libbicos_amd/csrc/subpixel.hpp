@@ -168,7 +168,9 @@ void subpixel_kernel(AgreeArgs a) {
                 if (v0_low || (a.has_minvar && v1 < minvar))
                     nxc = -1;
                 else
-                    nxc = div_p(cov, sqrt_p(v0 * v1));
+                    // v0, v1: 0 or >= (1/65)^2 (centred integer samples: |l - m| is 0 or
+                    // >= ~1/n), so their product is 0 or far above 2^-96
+                    nxc = div_p(cov, nxc::sqrt_p_var(v0 * v1));
                 if (best < nxc) {
                     best_x = x;
                     best = nxc;
