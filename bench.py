@@ -11,6 +11,14 @@ to rank 0 with ONE RCCL gather per step, inside the timed region; the gather of
 step k overlaps the kernels of step k+1 (double-buffered), and every gather has
 completed before the closing barrier.
 
+Frames in flight (--inflight F, default 2): step k runs on stream k % F with its own
+engine and output buffers, so consecutive frames overlap the way a camera stream is
+processed -- the HBM-bound transform / agree of one frame fill the compute-unit slots the
+previous frame's search leaves idle in its last round of workgroups (narrow row bands:
+192 rows at N = 8). Every step still does the whole match into its own buffers; `value`
+and `ms_per_step` are the throughput over the K steps, and `ms_per_match_one_at_a_time`
+is the latency of one match with nothing overlapping it (this rank's band, no gather).
+
 Extra keys on the JSON line:
   roofline      the dominant kernel (the Hamming search), timed live with HIP
                 events on the stream it runs on. Default (matrix-core search,
@@ -222,6 +230,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target wall time of the CPU baseline sample")
     ap.add_argument("--kernel-reps", type=int, default=10)
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight: step k runs on stream k %% F with its own engine, so "
+                         "one frame's HBM-bound stages fill the slots the previous frame's "
+                         "search leaves idle (1 = strictly one match after another)")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the end-to-end host-buffer measurement (rank 0, N=1)")
     ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
@@ -294,46 +306,58 @@ def main():
     s0 = torch.from_numpy(L).to(dev)
     s1 = torch.from_numpy(R).to(dev)
     del L, R
-    eng = device.Engine(local_dev)
+    F = max(1, args.inflight)
+    # one engine (workspace) and one stream per frame in flight; slot 0 = torch's stream
+    engines = [device.Engine(local_dev) for _ in range(F)]
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(F - 1)]
+    eng = engines[0]
     has_corr = mcfg.nxcorr_threshold is not None
-    out = torch.empty((rows, W), dtype=torch.float32 if has_corr else torch.int16, device=dev)
-    corr = torch.empty((rows, W), dtype=torch.float32, device=dev) if has_corr else None
+    outs = [torch.empty((rows, W), dtype=torch.float32 if has_corr else torch.int16, device=dev)
+            for _ in range(F)]
+    corrs = [torch.empty((rows, W), dtype=torch.float32, device=dev) if has_corr else None
+             for _ in range(F)]
+    out, corr = outs[0], corrs[0]
 
     gather = world > 1 and args.scaling == "strong"
     if gather:
         hb = band_height(H, world)
         # one packed [disparity | corrmap] band buffer -> ONE RCCL gather per step. The
-        # match writes straight into it (no copies), and two buffers alternate so step
-        # k's gather (RCCL stream) overlaps step k+1's kernels (compute stream).
+        # match writes straight into it (no copies); the buffers alternate (at least two, one
+        # per frame in flight) so step k's gather (RCCL stream) overlaps later steps' kernels.
         planes = 2 if has_corr else 1
         gdev = dev if args.backend == "nccl" else torch.device("cpu")
-        sends = [torch.zeros((planes, hb, W), dtype=torch.float32, device=gdev) for _ in range(2)]
+        NB = max(2, F)
+        sends = [torch.zeros((planes, hb, W), dtype=torch.float32, device=gdev) for _ in range(NB)]
         recvs = [[torch.empty_like(sends[0]) for _ in range(world)] if rank == 0 else None
-                 for _ in range(2)]
-        pending = [None, None]
+                 for _ in range(NB)]
+        pending = [None] * NB
     state = {"k": 0}
 
     def step():
-        if not gather:
-            eng.match(s0, s1, mcfg, out=out, corrmap=corr)
-            return
-        i = state["k"] % 2
+        k = state["k"]
         state["k"] += 1
-        if pending[i] is not None:
-            pending[i].wait()  # the compute stream waits for the gather that last read sends[i]
-        buf = sends[i]
-        if has_corr and args.backend == "nccl":
-            eng.match(s0, s1, mcfg, out=buf[0, :rows], corrmap=buf[1, :rows])
-        else:
-            eng.match(s0, s1, mcfg, out=out, corrmap=corr)
-            buf[0, :rows].copy_(out if has_corr else out.float())
-            if has_corr:
-                buf[1, :rows].copy_(corr)
-        pending[i] = dist.gather(buf, recvs[i], dst=0, async_op=True)
+        f = k % F  # frame slot: engine + stream
+        with torch.cuda.stream(streams[f]):
+            if not gather:
+                engines[f].match(s0, s1, mcfg, out=outs[f], corrmap=corrs[f])
+                return
+            i = k % NB
+            if pending[i] is not None:
+                pending[i].wait()  # this stream waits for the gather that last read sends[i]
+            buf = sends[i]
+            if has_corr and args.backend == "nccl":
+                engines[f].match(s0, s1, mcfg, out=buf[0, :rows], corrmap=buf[1, :rows])
+            else:
+                engines[f].match(s0, s1, mcfg, out=outs[f], corrmap=corrs[f])
+                buf[0, :rows].copy_(outs[f] if has_corr else outs[f].float())
+                if has_corr:
+                    buf[1, :rows].copy_(corrs[f])
+            # the collective is ordered after this stream's match
+            pending[i] = dist.gather(buf, recvs[i], dst=0, async_op=True)
 
     def drain():
         if gather:
-            for i in range(2):
+            for i in range(NB):
                 if pending[i] is not None:
                     pending[i].wait()
                     pending[i] = None
@@ -375,6 +399,18 @@ def main():
     frames_px = H * W * (world if args.scaling == "weak" else 1)
     value = frames_px * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
+
+    # one match at a time on one stream (this rank's band, no gather): the latency of a
+    # frame, reported beside the pipelined throughput
+    serial = []
+    for _ in range(3):
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(10):
+            eng.match(s0, s1, mcfg, out=out, corrmap=corr)
+        torch.cuda.synchronize(dev)
+        serial.append((time.perf_counter() - t1) / 10 * 1e3)
+    ms_serial = sorted(serial)[1]
 
     # ---- dominant kernel, timed live: HIP events on the stream the search runs on
     st = torch.cuda.current_stream(dev)
@@ -556,6 +592,8 @@ def main():
             "spinup_matches": spins,
             "warmup_ms": round(warm_ms, 1),
             "ms_per_step": round(ms_per_step, 4),
+            "frames_in_flight": F,
+            "ms_per_match_one_at_a_time": round(ms_serial, 4),
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": None,
