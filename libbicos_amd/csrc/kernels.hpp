@@ -119,6 +119,9 @@ struct MxGeometry {
     int keys;               // 1: one product + xor keys (cols <= 16384), 2: two products
     int ksteps;             // 64-bit K-steps multiplied (<= words / 2; 3 for 256-bit
                             // descriptors with <= 192 used bits)
+    int fk;                 // 1: float keys with the column in the free upper half of the
+                            // last K-step allowed (<= 64 ksteps - 32 used bits, cols <= 2048;
+                            // search_mx.hip KEYS 3, first-minimum searches only)
 };
 // bits: highest used descriptor bit + 1 when the bits above are known to be zero (0 =
 // all of them)

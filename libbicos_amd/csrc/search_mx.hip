@@ -53,6 +53,10 @@
 #ifndef BICOS_MX_PREFETCH
 #define BICOS_MX_PREFETCH 1
 #endif
+// 1: FK (KEYS 3) searches prefetch too
+#ifndef BICOS_MX_FK_PF
+#define BICOS_MX_FK_PF 0
+#endif
 
 namespace bicos_hip {
 
@@ -90,6 +94,20 @@ constexpr uint32_t XK_INF = 0x7F000000u;  // "no key yet"; stays huge under the 
 // 8223 - (col1 - B) -- which keeps both in [0, 16383] for cols <= 8160.
 constexpr int XKF_K0 = 8160;
 constexpr int XKF_MAX_COLS = 8160;
+// KEYS 3 (float keys, no C matrix): where the descriptors leave the upper lane half of the
+// last 64-bit K-step free (e.g. 256-bit words with <= 160 transform bits, cfg4's 154), that
+// half carries the column: the right operand holds the binary digits of col1 % 32 there
+// (FP4 1, 2, 4, 4+4, 4+4+4+4 in nine elements), the left operand is +1.0 (its descriptor bits
+// are 0), and the MFMA scales that half of the right operand by 2^-12. So D = x + (col1 %
+// 32) * 2^-12 with C = 0 (an inline constant): 16 VGPRs freer than the XK keys. The running
+// minimum is kept relative to the current block base B, D = x + (col1 - B) * 2^-12, moved by
+// -32 * 2^-12 per (ascending) block with one float subtract; |col1 - B| < 2048 keeps the
+// column term inside (-0.5, 0.5), so floats order by x first and then by col1 (the first
+// minimum, v_min3_f32), rint(D) = x, and (D - x) * 4096 = col1 - B exactly (|D| < 256 ->
+// ulp 2^-16). NoDuplicates keeps the XK keys (the last minimum needs the bit trick).
+constexpr int FK_MAX_COLS = 2048;
+constexpr float FK_EPS = 1.f / 4096.f;
+constexpr int FK_SCALE_E8M0 = 127 - 12;  // 2^-12
 
 // 32 descriptor bits -> 32 FP4 elements through a byte table: byte q of dword m holds bits
 // 8q + 2m (low nibble) and 8q + 2m + 1 (high nibble), i.e. dword m = v_perm of the 4-entry
@@ -138,11 +156,41 @@ __device__ __forceinline__ uint32_t max16(const v16f& d, uint32_t m) {
     return umax3(m, umax3(a0, a1, a2), umax3(a3, a4, k(15)));
 }
 
+// FK column digits of r = col1 % 32 as one lane's 32 FP4 elements (element k = nibble k):
+// 1.0 * bit0, 2.0 * bit1, 4.0 * bit2, 4.0 * bit3 (twice), 4.0 * bit4 (four times)
+__device__ __forceinline__ v4i fk_digits(int r) {
+    uint32_t w0 = 0, w1 = 0;
+    w0 |= (r & 1) ? 0x2u : 0u;
+    w0 |= (r & 2) ? 0x40u : 0u;
+    w0 |= (r & 4) ? 0x600u : 0u;
+    w0 |= (r & 8) ? 0x66000u : 0u;
+    w0 |= (r & 16) ? 0x66600000u : 0u;
+    w1 |= (r & 16) ? 0x6u : 0u;
+    return v4i{(int)w0, (int)w1, 0, 0};
+}
+
+__device__ __forceinline__ float fmin3(float a, float b, float c) {
+    return __builtin_fminf(__builtin_fminf(a, b), c);
+}
+// min over the 16 float keys of a D tile and m (v_min3_f32 tree)
+__device__ __forceinline__ float fmin16(const v16f& d, float m) {
+    const float a0 = fmin3(d[0], d[1], d[2]), a1 = fmin3(d[3], d[4], d[5]);
+    const float a2 = fmin3(d[6], d[7], d[8]), a3 = fmin3(d[9], d[10], d[11]);
+    const float a4 = fmin3(d[12], d[13], d[14]);
+    return fmin3(m, fmin3(a0, a1, a2), fmin3(a3, a4, d[15]));
+}
+
 __device__ __forceinline__ v16f mfma_fp4(v4i a, v4i b, v16f c) {
     const v8i a8 = {a[0], a[1], a[2], a[3], 0, 0, 0, 0};
     const v8i b8 = {b[0], b[1], b[2], b[3], 0, 0, 0, 0};
     // cbsz = blgp = 4: both operands FP4 e2m1; zero scales = the unscaled instruction
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 0, 0, 0);
+}
+// the same with E8M0 scales: sa for this lane's block of the right operand (A), 2^0 for B
+__device__ __forceinline__ v16f mfma_fp4_sa(v4i a, v4i b, v16f c, int sa) {
+    const v8i a8 = {a[0], a[1], a[2], a[3], 0, 0, 0, 0};
+    const v8i b8 = {b[0], b[1], b[2], b[3], 0, 0, 0, 0};
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, sa, 0, 127);
 }
 
 
@@ -156,7 +204,9 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 //           product), any width;
 //       1 = XK keys, blocks in ascending col1 order (cols <= 16384);
 //       2 = XK keys in any block order with the last-minimum work skipped where it cannot
-//           matter (NoDuplicates, cols <= 8160; see below).
+//           matter (NoDuplicates, cols <= 8160; see below);
+//       3 = FK float keys, column in the free K half, ascending, no NoDuplicates
+//           (cols <= 2048, see FK_EPS).
 // FUSE: 0 = int16 `out`; 1 / 2 = NXC agree fused into the epilogue on u8 / u16 stacks
 // (agree.hpp:53-93 for the pixels the lane owns; float disparity + corrmap, see SearchArgs).
 //
@@ -186,7 +236,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void search_mx_kernel(SearchArgs a) {
     static_assert(TF == 0 || WORDS <= 4, "fused transform: descriptors up to 128 bits");
     using TTF = typename tf_type<TF == 2 ? 2 : 1>::type;
-    constexpr bool XK = KEYS != 0;
+    constexpr bool FK = KEYS == 3;
+    static_assert(!FK || (!NODUPES && FUSE == 0 && TF == 0), "FK keys: first minimum only");
+    constexpr bool XK = KEYS == 1 || KEYS == 2;
     constexpr bool FREE = KEYS == 2;
     static_assert(!FREE || NODUPES, "KEYS 2 is the NoDuplicates search");
     constexpr int K0 = FREE ? XKF_K0 : XK_K0;
@@ -261,12 +313,13 @@ void search_mx_kernel(SearchArgs a) {
     // Only where the registers allow (paired NoDuplicates tiles, <= 2 K-steps): cfg2 -1.5 %,
     // cfg5 -1 %; with 3 K-steps the extra live fragments spill inside the loop (cfg4 2.3x
     // slower)
-    constexpr bool PREFETCH = XK && PAIRS && KS <= 2 && BICOS_MX_PREFETCH;
+    // (FK: the registers of the C matrix pay for the prefetched fragments at 3 K-steps)
+    constexpr bool PREFETCH = ((XK && PAIRS && KS <= 2) || (FK && BICOS_MX_FK_PF)) && BICOS_MX_PREFETCH;
     uint32_t m1[T], m2[T], mp[T / 2 > 0 ? T / 2 : 1];
     int b2[T];  // KEYS 2: the base m2[t] is relative to (wave-uniform)
 #pragma unroll
     for (int t = 0; t < T; ++t) {
-        m1[t] = XK ? XK_INF : KEY_NONE;
+        m1[t] = XK || FK ? XK_INF : KEY_NONE;  // (FK: a huge positive float)
         m2[t] = XK ? XK_INF : 0u;
         b2[t] = 0;
     }
@@ -278,11 +331,21 @@ void search_mx_kernel(SearchArgs a) {
 
     v16f d[T], e[T];
     // products of tile `tile` into accumulator slot `slot`
+    const int fk_sa = h ? FK_SCALE_E8M0 : 127;  // FK: the column half of the last step x 2^-12
     auto products = [&](int slot, const v4i* af, const v4i* an, const v16f& c1, const v16f& c2,
                         int tile) {
-        d[slot] = mfma_fp4(af[0], bf[tile][0], c1);
+        if constexpr (FK && KS == 1) {
+            d[slot] = mfma_fp4_sa(af[0], bf[tile][0], c1, fk_sa);
+        } else {
+            d[slot] = mfma_fp4(af[0], bf[tile][0], c1);
+        }
 #pragma unroll
-        for (int s = 1; s < KS; ++s) d[slot] = mfma_fp4(af[s], bf[tile][s], d[slot]);
+        for (int s = 1; s < KS; ++s) {
+            if (FK && s == KS - 1)
+                d[slot] = mfma_fp4_sa(af[s], bf[tile][s], d[slot], fk_sa);
+            else
+                d[slot] = mfma_fp4(af[s], bf[tile][s], d[slot]);
+        }
         if constexpr (NODUPES && !XK) {
             e[slot] = mfma_fp4(an[0], bf[tile][0], c2);
 #pragma unroll
@@ -319,6 +382,8 @@ void search_mx_kernel(SearchArgs a) {
                 m2[t] = min16(d[t], m2[t] + (uint32_t)(B - b2[t]), XK_COL);
                 b2[t] = B;
             }
+        } else if constexpr (FK) {
+            m1[t] = fbits(fmin16(d[t], bitsf(m1[t]) - 32.f * FK_EPS));
         } else if constexpr (XK) {
             m1[t] = min16(d[t], m1[t] - 32u, 0u);
             if constexpr (NODUPES) m2[t] = min16(d[t], m2[t] + 32u, XK_COL);
@@ -327,7 +392,7 @@ void search_mx_kernel(SearchArgs a) {
             if constexpr (NODUPES) m2[t] = max16(e[t], m2[t]);
         }
     };
-    int bprev = XK && !FREE ? -32 : 0;  // base of the previously reduced block
+    int bprev = (XK || FK) && !FREE ? -32 : 0;  // base of the previously reduced block
     // KEYS 2, tiles in pairs (2p, 2p+1) for block base B (accumulators dx, dy): ONE
     // v_permlane32_swap of the two block minima leaves tile 2p's both-halves minimum in
     // lanes 0-31 and tile 2p+1's in lanes 32-63 (swap: vdst lanes 32-63 <-> src lanes 0-31),
@@ -397,7 +462,10 @@ void search_mx_kernel(SearchArgs a) {
                     if (c1 < cols && w < WORDS) x = row1[(size_t)c1 * WORDS + w];
                 }
                 if (WORDS == 8 && KS == 4 && w == 7) x &= 0x7FFFFFFFu;
-                lds_mx[w * chunk + c] = expand_bits(x, LUT_A);
+                if (FK && w == WL - 1)  // (the descriptors leave this slot 0: host check)
+                    lds_mx[w * chunk + c] = fk_digits(c1 & 31);
+                else
+                    lds_mx[w * chunk + c] = expand_bits(x, LUT_A);
             }
         }
         if (expand) __syncthreads();
@@ -406,7 +474,10 @@ void search_mx_kernel(SearchArgs a) {
         const int nfull = ncols / 32;
         const bool partial = (ncols & 31) != 0;
         v16f cc;  // C of the current block: BIAS + col1 * EPS (XK: cx, the same for all)
-        if constexpr (XK) {
+        if constexpr (FK) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cc[r] = 0.f;  // C = 0: an inline constant
+        } else if constexpr (XK) {
             cc = cx;
         } else {
 #pragma unroll
@@ -545,14 +616,14 @@ void search_mx_kernel(SearchArgs a) {
                 if (b < 0) b += nfull;
                 block(b, cc, cc);
             }
-        } else if constexpr (XK && PREFETCH) {
+        } else if constexpr ((XK || FK) && PREFETCH) {
             v4i af[KS];
             if (nfull > 0) load_af(af, 0);
             for (int b = 0; b < nfull; ++b) block_pf(b, af, b + 1 < nfull ? b + 1 : -1);
             if (partial) partial_block(cc);
         } else {
             for (int b = 0; b < nfull; ++b) {
-                if constexpr (!XK) {
+                if constexpr (!XK && !FK) {
                     if (b) {
 #pragma unroll
                         for (int r = 0; r < 16; ++r) cc[r] += 32.f * KEY_EPS;  // exact (same binade)
@@ -561,7 +632,7 @@ void search_mx_kernel(SearchArgs a) {
                 block(b, cc, cc);
             }
             if (partial) {
-                if constexpr (!XK) {
+                if constexpr (!XK && !FK) {
                     if (nfull) {
 #pragma unroll
                         for (int r = 0; r < 16; ++r) cc[r] += 32.f * KEY_EPS;
@@ -579,6 +650,8 @@ void search_mx_kernel(SearchArgs a) {
         if constexpr (FREE) m2[t] += (uint32_t)(bprev - b2[t]);  // into the last block's frame
         if constexpr (PAIRS)  // already merged; valid in the half that writes tile t
             m1[t] = mp[t / 2];
+        else if constexpr (FK)
+            m1[t] = fbits(__builtin_fminf(bitsf(m1[t]), bitsf((uint32_t)__shfl_xor((int)m1[t], 32))));
         else
             m1[t] = min(m1[t], (uint32_t)__shfl_xor((int)m1[t], 32));
         if constexpr (NODUPES && XK) m2[t] = min(m2[t], (uint32_t)__shfl_xor((int)m2[t], 32));
@@ -587,6 +660,10 @@ void search_mx_kernel(SearchArgs a) {
     // best col1 of tile t, and whether it is the only column at the minimum cost
     // (XK: the minima are relative to the base of the last block reduced)
     auto best_of = [&](int t) {
+        if constexpr (FK) {
+            const float v = bitsf(m1[t]);
+            return bprev + (int)((v - __builtin_rintf(v)) * 4096.f);  // exact (see FK_EPS)
+        }
         return XK ? (int)(m1[t] & XK_COL) - K0 + bprev : key_col(m1[t]);
     };
     auto unique_of = [&](int t, int best) {
@@ -708,6 +785,9 @@ hipError_t launch_mx_t(const SearchArgs& a, const MxGeometry& g, hipStream_t st)
         return v && !std::strcmp(v, "natural");
     }();
     if (g.keys == 1) {
+        if constexpr (!NODUPES) {
+            if (g.fk) return launch_mx_k<WORDS, KSU, NODUPES, 3>(a, g, st);
+        }
         if constexpr (NODUPES) {
             if (a.cols <= XKF_MAX_COLS && !natural) return launch_mx_k<WORDS, KSU, NODUPES, 2>(a, g, st);
         }
@@ -732,6 +812,10 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     // step to drop (129..192 used bits)
     g.ksteps = words >= 2 ? words / 2 : 1;
     if (words == 8 && bits > 0 && bits <= 192) g.ksteps = 3;
+    // BICOS_MX_FK=0: XK keys for the first-minimum searches too (A/B; read per call)
+    const char* fk_v = std::getenv("BICOS_MX_FK");
+    const bool fk_env = !(fk_v && fk_v[0] == '0');
+    g.fk = fk_env && g.keys == 1 && bits > 0 && bits <= 64 * g.ksteps - 32 && cols <= FK_MAX_COLS;
     const int wl = 2 * g.ksteps;
     // LDS chunk of expanded right descriptors (16 B per word per col1), multiple of 32
     int chunk = lds_bytes / (wl * 16);

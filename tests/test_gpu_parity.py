@@ -395,6 +395,66 @@ def test_fused_transform_search_equals_separate(gpu, oracle, n, H, W, dt, kw, mo
         same(d_f, do)
 
 
+@pytest.mark.parametrize("n,H,W,dt,kw", [
+    (40, 6, 2048, np.uint8, dict(variant=1, max_lr_diff=1)),   # widest FK row (|col1 - B| < 2048)
+    (40, 3, 2049, np.uint8, dict(variant=1, max_lr_diff=1)),   # one column more: XK keys
+    (20, 4, 515, np.uint8, dict(variant=1, max_lr_diff=2, nxcorr_threshold=0.6)),  # 75 bits
+    (8, 5, 700, np.uint16, dict(variant=1, max_lr_diff=0)),    # 32-bit descriptors
+    (33, 4, 640, np.uint8, dict(variant=1, max_lr_diff=1)),    # 125 bits: no free half, XK
+])
+def test_fk_keys_equal_xk_keys(gpu, oracle, n, H, W, dt, kw, monkeypatch):
+    """KEYS 3 (float keys, the column carried in the free K half with an E8M0 scale of
+    2^-12, C = 0) against the XK keys (BICOS_MX_FK=0) and the oracle."""
+    L, R = stereo_stack(n, H, W, dt, dmin=2, drange=40, seed=n * 13 + W)
+    monkeypatch.setenv("BICOS_MX_FK", "0")
+    d_x, c_x = gpu_match(gpu, L, R, **kw)
+    monkeypatch.setenv("BICOS_MX_FK", "1")
+    d_f, c_f = gpu_match(gpu, L, R, **kw)
+    same(d_f, d_x)
+    if c_x is not None:
+        same(c_f, c_x)
+    do, _ = oracle.match(L, R, cfg_of(oracle, **kw))
+    same(d_f, do)
+
+
+@pytest.mark.parametrize("words,bits,W", [(8, 150, 2048), (8, 160, 1000), (4, 90, 777), (1, 32, 301)])
+def test_fk_search_ties(gpu, words, bits, W, monkeypatch):
+    """First-minimum search (flags 0) on low-entropy descriptors (few set bits: many equal
+    costs, so the lowest-col1 tie rule decides most pixels): FK keys == XK keys == numpy."""
+    import torch
+    rng = np.random.default_rng(words * 1000 + W)
+    rows = 3
+    nb = bits
+    pitch = gpu._L.bicos_desc_pitch(W, words)
+
+    def desc():
+        # AND of three random words: each bit set with p = 1/8 (low entropy, many ties)
+        w = rng.integers(0, 2**32, size=(3, rows, W, words), dtype=np.uint64)
+        v = (w[0] & w[1] & w[2]).astype(np.uint32)
+        for q in range(words):
+            lo = 32 * q
+            v[:, :, q] &= np.uint32(0 if lo >= nb else (0xFFFFFFFF if nb - lo >= 32 else (1 << (nb - lo)) - 1))
+        d = np.zeros((rows, pitch), np.uint32)
+        d[:, :W * words] = v.reshape(rows, W * words)
+        return d
+    d0, d1 = desc(), desc()
+    t0 = torch.from_numpy(d0.view(np.int32)).cuda()
+    t1 = torch.from_numpy(d1.view(np.int32)).cuda()
+    monkeypatch.setenv("BICOS_MX_FK", "0")
+    ox = host(gpu.search(t0, t1, W, words, flags=0, bits=bits))
+    monkeypatch.setenv("BICOS_MX_FK", "1")
+    of = host(gpu.search(t0, t1, W, words, flags=0, bits=bits))
+    same(of, ox)
+    # numpy: popcount Hamming, lowest col1 among the minima, disparity = col0 - col1
+    pc = np.array([bin(i).count("1") for i in range(256)], np.uint8)
+    for r in range(rows):
+        a = d0[r, :W * words].reshape(W, words).view(np.uint8).reshape(W, 1, words * 4)
+        b = d1[r, :W * words].reshape(W, words).view(np.uint8).reshape(1, W, words * 4)
+        ham = pc[a ^ b].sum(axis=2, dtype=np.int32)
+        exp = np.arange(W) - ham.argmin(axis=1)
+        assert np.array_equal(of[r].astype(np.int64), exp), r
+
+
 def test_errors(gpu):
     import torch
     from libbicos_amd import BicosError
