@@ -115,13 +115,19 @@ __device__ __forceinline__ void limited_descriptor(const StackReader<TIn>& rd, u
     const int n = EXACT ? MAXN : n_rt;
 
     uint32_t v[MAXN];
-    uint32_t sum = 0;
 #pragma unroll
     for (int t = 0; t < MAXN; ++t)
-        if (t < n) {
-            v[t] = rd((uint32_t)col, rowoff + (uint32_t)t * pp);
+        if (t < n) v[t] = rd((uint32_t)col, rowoff + (uint32_t)t * pp);
+    // the sum from the pair sums ps[t] = v[t] + v[t+1] of even t: the loop below compares
+    // those same pair sums (descriptor_transform.hpp:52-58), so they are computed once
+    uint32_t sum = 0;
+#pragma unroll
+    for (int t = 0; t < MAXN; t += 2) {
+        if (t + 1 < n)
+            sum += v[t] + v[t + 1];
+        else if (t < n)
             sum += v[t];
-        }
+    }
     const uint32_t q = __umulhi(sum, magic);
     const uint32_t thr = q + (q * (uint32_t)n != sum ? 1u : 0u);  // ceil(sum / n)
 
