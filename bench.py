@@ -240,6 +240,10 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (production); gloo = rehearsal of the N>1 "
                          "path with several ranks sharing one GPU (not a measurement)")
+    ap.add_argument("--verify-gather", action="store_true",
+                    help="after the timed run, rank 0 checks the last gathered frame (float "
+                         "disparity + corrmap, every band) against a one-GPU match of the "
+                         "whole frame, byte for byte (untimed)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` without torchrun: start the N ranks ourselves, before
@@ -319,18 +323,42 @@ def main():
     out, corr = outs[0], corrs[0]
 
     gather = world > 1 and args.scaling == "strong"
+    # integer disparities (NXC without subpixel): the band ships its disparity as int16 --
+    # (float) of it IS the float map -- and rank 0 converts the gathered frame back to float32
+    # with one op: 6 instead of 8 bytes per pixel over xGMI
+    i16 = has_corr and mcfg.subpixel_step is None
     if gather:
         hb = band_height(H, world)
-        # one packed [disparity | corrmap] band buffer -> ONE RCCL gather per step. The
-        # match writes straight into it (no copies); the buffers alternate (at least two, one
-        # per frame in flight) so step k's gather (RCCL stream) overlaps later steps' kernels.
-        planes = 2 if has_corr else 1
+        # one packed [disparity | corrmap] band buffer (bytes) -> ONE RCCL gather per step.
+        # The match writes straight into it (no copies); the buffers alternate (at least two,
+        # one per frame in flight) so step k's gather (RCCL stream) overlaps later steps'
+        # kernels.
+        dbytes = hb * W * (2 if i16 else 4)
+        off = (dbytes + 3) // 4 * 4
+        nbytes = off + (hb * W * 4 if has_corr else 0)
         gdev = dev if args.backend == "nccl" else torch.device("cpu")
         NB = max(2, F)
-        sends = [torch.zeros((planes, hb, W), dtype=torch.float32, device=gdev) for _ in range(NB)]
-        recvs = [[torch.empty_like(sends[0]) for _ in range(world)] if rank == 0 else None
-                 for _ in range(NB)]
+        sends = [torch.zeros(nbytes, dtype=torch.uint8, device=gdev) for _ in range(NB)]
+        recv_all = [torch.empty((world, nbytes), dtype=torch.uint8, device=gdev) if rank == 0
+                    else None for _ in range(NB)]
+        recvs = [list(r.unbind(0)) if r is not None else None for r in recv_all]
         pending = [None] * NB
+        frame_disp = torch.empty((world, hb, W), dtype=torch.float32, device=gdev) \
+            if rank == 0 and i16 else None
+
+        def disp_view(buf):  # [hb, W] disparity plane of a packed buffer (or [world, hb, W])
+            d = buf[..., :dbytes].view(torch.int16 if i16 else
+                                       (torch.float32 if has_corr else torch.int16))
+            return d.view(buf.shape[:-1] + (hb, W))
+
+        def corr_view(buf):
+            return buf[..., off:].view(torch.float32).view(buf.shape[:-1] + (hb, W))
+
+        def land(i):  # rank 0, gather i complete: the frame's float disparity map
+            pending[i].wait()
+            pending[i] = None
+            if rank == 0 and i16:
+                frame_disp.copy_(disp_view(recv_all[i]))
     state = {"k": 0}
 
     def step():
@@ -343,24 +371,24 @@ def main():
                 return
             i = k % NB
             if pending[i] is not None:
-                pending[i].wait()  # this stream waits for the gather that last read sends[i]
+                land(i)  # this stream waits for the gather that last read sends[i]
             buf = sends[i]
-            if has_corr and args.backend == "nccl":
-                engines[f].match(s0, s1, mcfg, out=buf[0, :rows], corrmap=buf[1, :rows])
+            if args.backend == "nccl":
+                engines[f].match(s0, s1, mcfg, out=disp_view(buf)[:rows],
+                                 corrmap=corr_view(buf)[:rows] if has_corr else None)
             else:
                 engines[f].match(s0, s1, mcfg, out=outs[f], corrmap=corrs[f])
-                buf[0, :rows].copy_(outs[f] if has_corr else outs[f].float())
+                disp_view(buf)[:rows].copy_(outs[f])
                 if has_corr:
-                    buf[1, :rows].copy_(corrs[f])
+                    corr_view(buf)[:rows].copy_(corrs[f])
             # the collective is ordered after this stream's match
             pending[i] = dist.gather(buf, recvs[i], dst=0, async_op=True)
 
     def drain():
         if gather:
-            for i in range(NB):
-                if pending[i] is not None:
-                    pending[i].wait()
-                    pending[i] = None
+            for k in range(state["k"] - NB, state["k"]):  # oldest gather first
+                if k >= 0 and pending[k % NB] is not None:
+                    land(k % NB)
 
     # Untimed warm-up. First a clock spin-up: at least --spinup-ms of back-to-back local
     # matches (no collectives, so ranks need not agree on a count). The GPU's clocks ramp
@@ -395,6 +423,26 @@ def main():
                          device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+
+    if gather and args.verify_gather and rank == 0:
+        # every gather has landed (drain): slot (K-1) % NB holds the last step's frame
+        last = (state["k"] - 1) % NB
+        FL, FR = stereo_stack(n, H, W, np.uint8, row_begin=0, row_end=H)
+        fd, fc = eng.match(torch.from_numpy(FL).to(dev), torch.from_numpy(FR).to(dev), mcfg)
+        fd = fd.float().cpu() if not has_corr else fd.cpu()
+        got_d = (frame_disp if i16 else disp_view(recv_all[last])).float().cpu()
+        for r in range(world):
+            rb, re_ = band_rows(H, world, r)
+            if not torch.equal(got_d[r, :re_ - rb].view(torch.int32) if has_corr else
+                               got_d[r, :re_ - rb], fd[rb:re_].view(torch.int32) if has_corr
+                               else fd[rb:re_]):
+                raise SystemExit("verify-gather: disparity band %d differs" % r)
+            if has_corr and not torch.equal(
+                    corr_view(recv_all[last])[r, :re_ - rb].cpu().view(torch.int32),
+                    fc[rb:re_].cpu().view(torch.int32)):
+                raise SystemExit("verify-gather: corrmap band %d differs" % r)
+        print("verify-gather: %d bands byte-identical to the whole-frame match" % world,
+              file=sys.stderr)
 
     frames_px = H * W * (world if args.scaling == "weak" else 1)
     value = frames_px * args.steps / elapsed / 1e6

@@ -141,6 +141,19 @@ int bicos_match_device(bicos_engine* e, const void* stack0, const void* stack1, 
                        void* stream);
 
 /*
+ * bicos_match_device with the disparity map always int16, also with the NXC stage: the
+ * integer disparity, -32768 where invalid or below the threshold, so that
+ * (float)disparity is exactly the float32 map bicos_match_device writes (the reference's
+ * float map is the int16 one converted, src/impl/cpu.cpp:77-95). Half the bytes of the
+ * float map -- what a row band ships to the gathering GPU (bench.py). A subpixel config
+ * is rejected (BICOS_E_ARG): its disparities are not integers. No reference counterpart.
+ */
+int bicos_match_device_i16(bicos_engine* e, const void* stack0, const void* stack1, int n,
+                           int rows, int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                           const BicosConfig* cfg, int has_nxcorr, void* disparity, void* corrmap,
+                           void* stream);
+
+/*
  * Full match on host buffers (the reference's cv::Mat path; what BICOS_Match and
  * pybicos.match run). Synchronous.
  *   e             : engine, or NULL for the current device's default engine

@@ -56,7 +56,7 @@ EXPORTS = (
     "BICOS_CreateDefaultConfig", "BICOS_FreeConfig", "BICOS_FreeResult", "BICOS_Match",
     "BICOS_InvalidDisparityFloat", "BICOS_InvalidDisparityInt16", "bicos_last_error",
     "bicos_engine_create", "bicos_engine_default", "bicos_engine_destroy", "bicos_engine_tune", "bicos_descriptor_words", "bicos_output_type",
-    "bicos_match_device", "bicos_match_host", "bicos_match_host_multi", "bicos_match_bands_device",
+    "bicos_match_device", "bicos_match_device_i16", "bicos_match_host", "bicos_match_host_multi", "bicos_match_bands_device",
     "bicos_desc_pitch", "bicos_transform_device", "bicos_search_device",
     "bicos_agree_device", "bicos_subpixel_device", "bicos_search_agree_device", "bicos_build_info",
 )
@@ -120,6 +120,8 @@ def lib() -> ctypes.CDLL:
     L.bicos_match_device.argtypes = [P, P, P, I, I, I, Z, Z, I, ctypes.POINTER(BicosConfig), I,
                                      P, P, P]
     L.bicos_match_device.restype = I
+    L.bicos_match_device_i16.argtypes = L.bicos_match_device.argtypes
+    L.bicos_match_device_i16.restype = I
     L.bicos_match_host.argtypes = [P, PP, PP, I, I, I, Z, I, ctypes.POINTER(BicosConfig), I, P, P]
     L.bicos_match_host.restype = I
     PZ = ctypes.POINTER(ctypes.c_size_t)

@@ -211,7 +211,8 @@ static int stack_span(int n, int rows, int cols, size_t row_pitch, size_t plane_
 
 int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int rows, int cols,
                  size_t row_pitch, size_t plane_pitch, int depth, const BicosConfig& cfg,
-                 bool has_nxcorr, float threshold, void* disp, void* corr, hipStream_t st) {
+                 bool has_nxcorr, float threshold, void* disp, void* corr, hipStream_t st,
+                 bool disp_i16) {
     if (!e) return fail(BICOS_E_ARG, "null engine");
     if (n < 2) return fail(BICOS_E_ARG, "need at least two images");
     if (depth != 1 && depth != 2)
@@ -232,6 +233,8 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     const int nsteps = has_step ? subpixel_steps(cfg.subpixel_step) : 0;
     if (has_step && !nsteps)
         return fail(BICOS_E_ARG, "subpixel_step too small (more than 65536 interpolation steps)");
+    if (disp_i16 && has_step)
+        return fail(BICOS_E_ARG, "an int16 disparity map cannot hold subpixel disparities");
     if (rows == 0 || cols == 0) return BICOS_OK;
     if (!s0 || !s1 || !disp) return fail(BICOS_E_ARG, "null buffer");
     if (row_pitch < (size_t)cols || plane_pitch < (size_t)rows * row_pitch)
@@ -309,7 +312,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
         return 1;
     }();
     const bool has_step_ = has_nxcorr && cfg.subpixel_step >= 0;
-    const bool fuse_agree = fuse_env && !consistency && has_nxcorr && !has_step_ && !dbl &&
+    const bool fuse_agree = fuse_env && !consistency && has_nxcorr && !has_step_ && !dbl && !disp_i16 &&
                             (mx ? fuse_env == 2 : g.variant == 16);
     if (fuse_agree && !fuse_tf) {
         bicos_hip::SearchArgs sa{d0, d1, nullptr, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
@@ -405,7 +408,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     aa.has_minvar = cfg.min_variance >= 0;
     aa.minvar = aa.has_minvar ? cfg.min_variance * (float)n : 0.f;  // cpu.cpp:127
     aa.out = disp;
-    aa.out_f32 = 1;
+    aa.out_f32 = disp_i16 ? 0 : 1;
     aa.corrmap = corr;
     aa.stack_bytes = span;
     if (has_step)
@@ -768,10 +771,11 @@ size_t bicos_desc_pitch(int cols, int words) {
     return ((size_t)cols * words + 3) / 4 * 4;
 }
 
-int bicos_match_device(bicos_engine* e, const void* stack0, const void* stack1, int n, int rows,
+namespace {
+int match_device_entry(bicos_engine* e, const void* stack0, const void* stack1, int n, int rows,
                        int cols, size_t row_pitch, size_t plane_pitch, int depth,
                        const BicosConfig* cfg, int has_nxcorr, void* disparity, void* corrmap,
-                       void* stream) {
+                       void* stream, bool disp_i16) {
     if (!cfg) return fail(BICOS_E_ARG, "null config");
     if (!e) return fail(BICOS_E_ARG, "null engine");
     try {
@@ -781,12 +785,29 @@ int bicos_match_device(bicos_engine* e, const void* stack0, const void* stack1, 
         // reference src/pybicos_c.cpp:59-61: a negative threshold keeps the default 0.5
         const float thr = cfg->nxcorr_threshold >= 0 ? cfg->nxcorr_threshold : 0.5f;
         return match_device(e, stack0, stack1, n, rows, cols, row_pitch, plane_pitch, depth, *cfg,
-                            has_nxcorr != 0, thr, disparity, corrmap, (hipStream_t)stream);
+                            has_nxcorr != 0, thr, disparity, corrmap, (hipStream_t)stream, disp_i16);
     } catch (const std::exception& ex) {
         return fail(BICOS_E_INTERNAL, ex.what());
     } catch (...) {
         return fail(BICOS_E_INTERNAL, "unknown exception");
     }
+}
+}  // namespace
+
+int bicos_match_device(bicos_engine* e, const void* stack0, const void* stack1, int n, int rows,
+                       int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                       const BicosConfig* cfg, int has_nxcorr, void* disparity, void* corrmap,
+                       void* stream) {
+    return match_device_entry(e, stack0, stack1, n, rows, cols, row_pitch, plane_pitch, depth, cfg,
+                              has_nxcorr, disparity, corrmap, stream, false);
+}
+
+int bicos_match_device_i16(bicos_engine* e, const void* stack0, const void* stack1, int n, int rows,
+                           int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                           const BicosConfig* cfg, int has_nxcorr, void* disparity, void* corrmap,
+                           void* stream) {
+    return match_device_entry(e, stack0, stack1, n, rows, cols, row_pitch, plane_pitch, depth, cfg,
+                              has_nxcorr, disparity, corrmap, stream, true);
 }
 
 int bicos_match_host(bicos_engine* e, const void* const* stack0, const void* const* stack1, int n,

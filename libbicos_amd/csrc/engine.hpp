@@ -94,10 +94,12 @@ bool fused_consistency();
 bicos_hip::SearchGeometry geometry_lr(const bicos_engine* e, int rows, int cols, int words,
                                       bool nodupes);
 
-// Full match on device buffers (validated arguments). corr may be null.
+// Full match on device buffers (validated arguments). corr may be null. disp_i16: the
+// disparity map is int16 even with the NXC stage (no subpixel; bicos_match_device_i16).
 int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int rows, int cols,
                  size_t row_pitch, size_t plane_pitch, int depth, const BicosConfig& cfg,
-                 bool has_nxcorr, float threshold, void* disp, void* corr, hipStream_t st);
+                 bool has_nxcorr, float threshold, void* disp, void* corr, hipStream_t st,
+                 bool disp_i16 = false);
 
 // Host buffers in and out (the reference's cv::Mat path, src/impl/cpu.cpp:100-159): the
 // stacks are uploaded in row bands through pinned slots on a copy stream while earlier

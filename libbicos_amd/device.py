@@ -130,7 +130,11 @@ class Engine:
               out: Optional[torch.Tensor] = None, corrmap: Optional[torch.Tensor] = None,
               stream=None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
         """Full BICOS::match on device stacks. Returns (disparity, corrmap) on the
-        device; asynchronous on `stream` (default: torch's current stream)."""
+        device; asynchronous on `stream` (default: torch's current stream).
+
+        With the NXC stage and no subpixel step, `out` may also be an int16 tensor: the
+        integer disparity map (bicos_match_device_i16), whose float32 conversion is exactly
+        the float map -- half the bytes, e.g. for a row band that is gathered elsewhere."""
         cfg = cfg or MatchConfig()
         n, rows, cols, rp, pp = _check_stack(stack0)
         if tuple(stack1.shape) != (n, rows, cols) or stack1.stride() != stack0.stride() or \
@@ -140,6 +144,10 @@ class Engine:
         dev = stack0.device
         disp_dtype = torch.float32 if has_nxcorr else torch.int16
         corr_dtype = torch.float64 if cfg.precision else torch.float32
+        i16 = (out is not None and has_nxcorr and out.dtype == torch.int16 and
+               cfg.subpixel_step is None)
+        if i16:
+            disp_dtype = torch.int16
         if out is None:
             out = torch.empty((rows, cols), dtype=disp_dtype, device=dev)
         _check_out(out, "out", (rows, cols), (disp_dtype,), dev)
@@ -149,7 +157,8 @@ class Engine:
             corrmap = None
         if corrmap is not None:
             _check_out(corrmap, "corrmap", (rows, cols), (corr_dtype,), dev)
-        rc = self._L.bicos_match_device(
+        entry = self._L.bicos_match_device_i16 if i16 else self._L.bicos_match_device
+        rc = entry(
             self._h, stack0.data_ptr(), stack1.data_ptr(), n, rows, cols, rp, pp, _depth(stack0),
             ctypes.byref(c), has_nxcorr, out.data_ptr(),
             corrmap.data_ptr() if corrmap is not None else None, _stream(dev, stream))

@@ -729,3 +729,51 @@ def test_padded_pitch_odd_width(gpu, oracle, W, P, dt):
         same(host(d), rd)
         if rc is not None:
             same(host(c), rc)
+
+
+# ------------------------------- int16 disparity with the NXC stage (bicos_match_device_i16)
+# (float) of the int16 map is the float32 map byte for byte, the corrmap is unchanged, for
+# every variant without subpixel; a subpixel config is rejected. The second half writes into
+# views of one packed uint8 band buffer, exactly as bench.py's gather path does.
+@pytest.mark.parametrize("n,H,W,dt,kw", [
+    (33, 9, 2048, np.uint8, dict(nxcorr_threshold=0.96)),
+    (17, 5, 1300, np.uint16, dict(nxcorr_threshold=0.8, min_variance=1.5)),
+    (40, 4, 900, np.uint8, dict(nxcorr_threshold=0.9, variant=1, max_lr_diff=1)),
+    (8, 7, 640, np.uint8, dict(nxcorr_threshold=0.9, precision=1)),
+])
+def test_int16_disparity_entry(gpu, n, H, W, dt, kw):
+    import torch
+    from libbicos_amd.device import MatchConfig
+    L, R = stereo_stack(n, H, W, dt, dmin=3, drange=30, seed=n + H)
+    L[:, 1, 100:140] = 7  # flat patch: NaN correlations pass the threshold
+    s0, s1 = dev(L), dev(R)
+    cfg = MatchConfig(**kw)
+    fo, fc = gpu.match(s0, s1, cfg)
+    io = torch.empty((H, W), dtype=torch.int16, device="cuda")
+    io, ic = gpu.match(s0, s1, cfg, out=io)
+    assert io.dtype == torch.int16
+    same(host(io).astype(np.float32), host(fo))
+    same(host(ic), host(fc))
+    if kw.get("precision"):
+        return
+    # packed [int16 disparity | pad | float32 corrmap] band buffer of hb >= H rows
+    hb = H + 1
+    dbytes = hb * W * 2
+    off = (dbytes + 3) // 4 * 4
+    buf = torch.full((off + hb * W * 4,), 0xAB, dtype=torch.uint8, device="cuda")
+    dv = buf[:dbytes].view(torch.int16).view(hb, W)
+    cv = buf[off:].view(torch.float32).view(hb, W)
+    gpu.match(s0, s1, cfg, out=dv[:H], corrmap=cv[:H])
+    same(host(dv[:H]), host(io))
+    same(host(cv[:H]), host(ic))
+    assert (host(buf[H * W * 2:off]) == 0xAB).all()  # nothing written past the band
+    assert (host(buf[off + H * W * 4:]) == 0xAB).all()
+
+
+def test_int16_disparity_rejects_subpixel(gpu):
+    import torch
+    from libbicos_amd.device import MatchConfig
+    L, R = stereo_stack(8, 16, 64)
+    with pytest.raises(ValueError):
+        gpu.match(dev(L), dev(R), MatchConfig(subpixel_step=0.1),
+                  out=torch.empty((16, 64), dtype=torch.int16, device="cuda"))
