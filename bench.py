@@ -333,7 +333,7 @@ def main():
         # The match writes straight into it (no copies); the buffers alternate (at least two,
         # one per frame in flight) so step k's gather (RCCL stream) overlaps later steps'
         # kernels.
-        dbytes = hb * W * (2 if i16 else 4)
+        dbytes = hb * W * (4 if has_corr and not i16 else 2)  # float map only with subpixel
         off = (dbytes + 3) // 4 * 4
         nbytes = off + (hb * W * 4 if has_corr else 0)
         gdev = dev if args.backend == "nccl" else torch.device("cpu")
