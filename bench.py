@@ -11,7 +11,7 @@ to rank 0 with ONE RCCL gather per step, inside the timed region; the gather of
 step k overlaps the kernels of step k+1 (double-buffered), and every gather has
 completed before the closing barrier.
 
-Frames in flight (--inflight F, default 2): step k runs on stream k % F with its own
+Frames in flight (--inflight F, default 3): step k runs on stream k % F with its own
 engine and output buffers, so consecutive frames overlap the way a camera stream is
 processed -- the HBM-bound transform / agree of one frame fill the compute-unit slots the
 previous frame's search leaves idle in its last round of workgroups (narrow row bands:
@@ -230,7 +230,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0,
                     help="target wall time of the CPU baseline sample")
     ap.add_argument("--kernel-reps", type=int, default=10)
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="frames in flight: step k runs on stream k %% F with its own engine, so "
                          "one frame's HBM-bound stages fill the slots the previous frame's "
                          "search leaves idle (1 = strictly one match after another)")

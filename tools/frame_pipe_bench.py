@@ -29,19 +29,22 @@ def main():
     ap.add_argument("--ns", default="1,8")
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--streams", default="1,2", help="stream counts S to compare")
     args = ap.parse_args()
+    Ss = [int(v) for v in args.streams.split(",")]
+    SM = max(Ss + [2])
     C = bench.CONFIGS[args.config]
     n, H, W = C["n"], C["H"], C["W"]
     mcfg = device.MatchConfig(**C["cfg"])
-    engines = [device.Engine(0), device.Engine(0)]
-    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    engines = [device.Engine(0) for _ in range(SM)]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(SM - 1)]
     for N in [int(v) for v in args.ns.split(",")]:
         b, e = band_rows(H, N, 0)
         rows = e - b
         L, R = stereo_stack(n, H, W, np.uint8, row_begin=b, row_end=e)
         s0, s1 = torch.from_numpy(L).cuda(), torch.from_numpy(R).cuda()
         outs = [(torch.empty((rows, W), dtype=torch.float32, device="cuda"),
-                 torch.empty((rows, W), dtype=torch.float32, device="cuda")) for _ in range(2)]
+                 torch.empty((rows, W), dtype=torch.float32, device="cuda")) for _ in range(SM)]
 
         def run(S, reps):
             for k in range(reps):
@@ -56,13 +59,13 @@ def main():
         t_end = time.perf_counter() + 0.15
         while time.perf_counter() < t_end:
             run(1, 4)
-        res = {1: [], 2: []}
+        res = {S: [] for S in Ss}
         for _ in range(args.rounds):
-            for S in (1, 2):
+            for S in Ss:
                 t0 = time.perf_counter()
                 run(S, args.reps)
                 res[S].append((time.perf_counter() - t0) / args.reps * 1e3)
-        for S in (1, 2):
+        for S in Ss:
             print(json.dumps({"config": args.config, "N": N, "band_rows": rows, "streams": S,
                               "ms_per_frame": round(statistics.median(res[S]), 4),
                               "ms_min": round(min(res[S]), 4)}), flush=True)
