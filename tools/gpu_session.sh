@@ -119,6 +119,10 @@ for step in "$@"; do
             done ;;
         profcfg)  # rocprofv3 kernel stats of one config (SC=cfgN)
             run prof_${SC:-cfg2} 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_${SC:-cfg2} -o run --output-format csv -- python bench.py --config ${SC:-cfg2} --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
+        profiso)  # rocprofv3 kernel stats with one frame at a time (no cross-frame kernel overlap), SCS="cfg2 cfg3 ..."
+            for c in ${SCS:-cfg2}; do
+                run profiso_$c 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profiso_$c -o run --output-format csv -- python bench.py --config $c --steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --no-host-path
+            done ;;
         *) echo "unknown step $step" ;;
     esac
 done
