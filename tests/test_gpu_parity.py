@@ -688,6 +688,32 @@ def test_default_engine_two_threads(gpu, oracle):
     assert not errors, errors
 
 
+def test_one_engine_alternating_streams(gpu, oracle):
+    """One engine, frames enqueued back to back with no host sync on streams 0,1,1,0,2,...:
+    the workspace wait is skipped when the previous use was on the same stream and kept
+    across streams (and across a workspace growth in the middle) -- every map exact."""
+    import torch
+    from libbicos_amd import device
+    cfg = dict(nxcorr_threshold=0.9)
+    frames = [stereo_stack(8, 48, 640, seed=21), stereo_stack(33, 40, 1300, seed=22),
+              stereo_stack(12, 56, 900, seed=23)]
+    refs = [oracle.match(L, R, oracle.OracleConfig(**cfg)) for L, R in frames]
+    devs = [(dev(L), dev(R)) for L, R in frames]
+    eng = device.Engine()
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream(), torch.cuda.Stream()]
+    order = [0, 1, 1, 0, 2, 2, 1, 0, 0, 2, 1, 2]
+    outs = []
+    torch.cuda.synchronize()
+    for k, si in enumerate(order):
+        f = k % len(frames)
+        with torch.cuda.stream(streams[si]):
+            outs.append((f, eng.match(devs[f][0], devs[f][1], device.MatchConfig(**cfg))))
+    torch.cuda.synchronize()
+    for f, (d, c) in outs:
+        same(host(d), refs[f][0])
+        same(host(c), refs[f][1])
+
+
 def test_device_outputs_are_validated(gpu):
     import torch
     from libbicos_amd.device import MatchConfig

@@ -123,6 +123,15 @@ for step in "$@"; do
             for c in ${SCS:-cfg2}; do
                 run profiso_$c 600 rocprofv3 --kernel-trace --stats -d gpurun_out/profiso_$c -o run --output-format csv -- python bench.py --config $c --steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --no-host-path
             done ;;
+        abpipe)  # frame pipeline (N=1 and N=8 bands, 1 and 3 streams): current lib vs build/alt.so, interleaved twice
+            cp libbicos_amd/libbicos_amd.so build/cur.so
+            for k in 1 2; do
+                cp build/cur.so libbicos_amd/libbicos_amd.so
+                run abpipe_cur$k 300 python tools/frame_pipe_bench.py --ns 1,8 --streams 1,3 --rounds 2
+                cp build/alt.so libbicos_amd/libbicos_amd.so
+                run abpipe_alt$k 300 python tools/frame_pipe_bench.py --ns 1,8 --streams 1,3 --rounds 2
+            done
+            cp build/cur.so libbicos_amd/libbicos_amd.so ;;
         *) echo "unknown step $step" ;;
     esac
 done
