@@ -77,6 +77,15 @@ CONFIGS = {
                        "without Consistency; not a BASELINE config)"),
     "cfg5": dict(n=33, H=2160, W=3840, dtype="u8", cfg=dict(nxcorr_threshold=0.96),
                  desc="33x2 @ 3840x2160 u8, 128-bit, nxcorr 0.96"),
+    # the reference README's published full match (README.md:80,90: ~44 ms on an RTX 4090,
+    # dataset 3208x2200 per example-disp.png): bicos-cli --limited --threshold 0.96
+    # --stacksize 33 --variance 2.0 --step 0.1
+    "readme": dict(n=33, H=2200, W=3208, dtype="u8",
+                   cfg=dict(nxcorr_threshold=0.96, min_variance=2.0, subpixel_step=0.1),
+                   desc="33x2 @ 3208x2200 u8, LIMITED 128-bit, nxcorr 0.96, min-variance 2.0, "
+                        "subpixel 0.1 (reference README.md:80,90 full match)",
+                   published={"ms_per_match": 44.0, "hardware": "RTX 4090",
+                              "source": "reference README.md:90 (~44 ms)"}),
 }
 
 
@@ -142,14 +151,27 @@ def mx_ksteps(words: int, bits: int) -> int:
     return ks
 
 
-def mx_flops(rows: int, W: int, words: int, cfg: dict, bits: int = 0):
-    """(algorithmic, executed) FLOPs of the matrix-core search per launch. Each Hamming
-    pair is a K-long dot product, K = descriptor bits (2K FLOPs); the MFMA executes the
-    K-steps that hold used bits (mx_ksteps). Consistency runs the forward and the reverse
-    search."""
+def mx_flops(rows: int, W: int, words: int, cfg: dict, bits: int = 0, set_bits: int = 0):
+    """(algorithmic, used-bit) FLOPs of the matrix-core search per launch. Each Hamming pair
+    is a K-long dot product (2K FLOPs). Algorithmic K = the descriptor bits the kernel
+    multiplies: the descriptor type's width (128 for u128, the reference's popcount width),
+    or fewer when whole 64-bit K-steps above the used bits are skipped (cfg4: 192 of 256;
+    mx_ksteps) -- never more than executed. Used-bit K = the bits the transform actually
+    sets (4n-6 LIMITED: 126 at n = 33, 154 at n = 40), the stricter view. Consistency runs
+    the forward and the reverse search."""
     passes = 2 if cfg.get("variant", 0) == 1 else 1
     pairs = search_pairs(rows, W, cfg) * passes
-    return pairs * 2 * 32 * words, pairs * 2 * 64 * mx_ksteps(words, bits)
+    k_exec = min(32 * words, 64 * mx_ksteps(words, bits))
+    k_used = min(k_exec, set_bits) if set_bits else k_exec
+    return pairs * 2 * k_exec, pairs * 2 * k_used
+
+
+def transform_bits(n: int, mode: int) -> int:
+    """Descriptor bits the transform sets: LIMITED 4n-6 (n >= 4; 7 / 4 for n = 3 / 2), FULL
+    n^2-2n+3 (descriptor_transform.hpp:31-123; tests/test_oracle.py pins both)."""
+    if mode:
+        return n * n - 2 * n + 3
+    return 4 * n - 6 if n >= 4 else (7 if n == 3 else 4)
 
 
 def mx_key_pair_peak(words: int, cfg: dict) -> float:
@@ -163,22 +185,47 @@ def mx_key_pair_peak(words: int, cfg: dict) -> float:
     return 1.0 / (full / (VALU_FULL_TOPS * 1e12) + half / (VALU_HALF_TOPS * 1e12))
 
 
-def load_traffic(kernel_prefix: str, rows: int, W: int):
-    """Per-launch HBM bytes of the search kernel from the committed PMC summary (the
-    latest profiles/pmc_r*.json whose grid matches), or None."""
+def kernel_source_hash() -> str:
+    """sha256 over the HIP kernel and host sources of libbicos_amd.so (csrc/, sorted). The PMC
+    summaries record it (tools/pmc_summary.py), and a bench line cites their HBM bytes only
+    when they were measured on the very sources it runs."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")))
-    for f in reversed(files):
+    import hashlib
+    h = hashlib.sha256()
+    for f in sorted(glob.glob(os.path.join(ROOT, "libbicos_amd", "csrc", "*"))):
+        if f.rsplit(".", 1)[-1] in ("hip", "hpp", "cpp", "h") or f.endswith("Makefile"):
+            h.update(os.path.basename(f).encode())
+            h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def load_traffic(kernel_prefix: str, config: str, rows: int):
+    """Per-launch HBM bytes (PMC FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections) of a kernel
+    from the committed profiles/pmc_r*.json entry for this config and row count, measured on
+    the current sources (kernel_source_hash). Returns {"bytes", "source"}, or {"bytes": None,
+    "why": ...} when no such profile exists."""
+    import glob
+    want = kernel_source_hash()
+    stale = None
+    for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")))):
         try:
             d = json.load(open(f))
         except Exception:
             continue
         for key, c in d.get("kernels", {}).items():
-            if key.startswith(kernel_prefix) and "hbm_read_bytes" in c and "hbm_write_bytes" in c \
-                    and c.get("rows") in (None, rows):
-                return {"bytes": c["hbm_read_bytes"] + c["hbm_write_bytes"],
-                        "source": os.path.relpath(f, ROOT) + " :: " + key}
-    return None
+            if c.get("config") != config or c.get("rows") != rows or \
+                    not c.get("kernel", "").startswith(kernel_prefix) or \
+                    "hbm_read_bytes" not in c or "hbm_write_bytes" not in c:
+                continue
+            src = os.path.relpath(f, ROOT) + " :: " + key
+            if d.get("source_sha") != want:
+                stale = stale or src
+                continue
+            return {"bytes": c["hbm_read_bytes"] + c["hbm_write_bytes"],
+                    "read_bytes": c["hbm_read_bytes"], "write_bytes": c["hbm_write_bytes"],
+                    "source": src, "source_sha": want}
+    return {"bytes": None, "why": ("PMC profile %s was taken on other sources" % stale) if stale
+            else "no PMC profile for %s rows=%d" % (config, rows), "source_sha": want}
 
 
 def launch_ranks(world: int) -> int:
@@ -246,9 +293,15 @@ def main():
                     help="nccl = RCCL over xGMI (production); gloo = rehearsal of the N>1 "
                          "path with several ranks sharing one GPU (not a measurement)")
     ap.add_argument("--verify-gather", action="store_true",
-                    help="after the timed run, rank 0 checks the last gathered frame (float "
-                         "disparity + corrmap, every band) against a one-GPU match of the "
-                         "whole frame, byte for byte (untimed)")
+                    help="(default; kept for old command lines) verify the gathered frames")
+    ap.add_argument("--no-verify-gather", action="store_true",
+                    help="skip the untimed check of the gathered frames (by default, after the "
+                         "timed run, NB more steps land over a sentinel and rank 0 checks every "
+                         "gather slot's whole frame against the oracle's sha256 in "
+                         "tests/golden/frames.json, or a one-GPU match of the whole frame)")
+    ap.add_argument("--band-of", type=int, default=1,
+                    help="one process, band 0 of an N-way row split (no gather): the band a "
+                         "rank of an N-GPU run computes, for profiling at band sizes")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` without torchrun: start the N ranks ourselves, before
@@ -308,6 +361,10 @@ def main():
         b, e = band_rows(H, world, rank)
     else:
         b, e = 0, H
+    if args.band_of > 1:
+        if world != 1:
+            raise SystemExit("--band-of is a one-process profiling mode")
+        b, e = band_rows(H, args.band_of, 0)
     rows = e - b
 
     # synthetic stacks of this rank's band, generated on the host once, resident in HBM
@@ -328,6 +385,7 @@ def main():
     out, corr = outs[0], corrs[0]
 
     gather = world > 1 and args.scaling == "strong"
+    nccl = args.backend == "nccl"
     # integer disparities (NXC without subpixel): the band ships its disparity as int16 --
     # (float) of it IS the float map -- and rank 0 converts the gathered frame back to float32
     # with one op: 6 instead of 8 bytes per pixel over xGMI
@@ -341,15 +399,17 @@ def main():
         dbytes = hb * W * (4 if has_corr and not i16 else 2)  # float map only with subpixel
         off = (dbytes + 3) // 4 * 4
         nbytes = off + (hb * W * 4 if has_corr else 0)
-        gdev = dev if args.backend == "nccl" else torch.device("cpu")
+        gdev = dev if nccl else torch.device("cpu")
         NB = max(2, F)
         sends = [torch.zeros(nbytes, dtype=torch.uint8, device=gdev) for _ in range(NB)]
         recv_all = [torch.empty((world, nbytes), dtype=torch.uint8, device=gdev) if rank == 0
                     else None for _ in range(NB)]
         recvs = [list(r.unbind(0)) if r is not None else None for r in recv_all]
         pending = [None] * NB
-        frame_disp = torch.empty((world, hb, W), dtype=torch.float32, device=gdev) \
-            if rank == 0 and i16 else None
+        # rank 0: the float32 disparity frame of each gather slot (one per slot,
+        # so a stale or misordered landing cannot hide behind a shared buffer)
+        frame_disps = [torch.empty((world, hb, W), dtype=torch.float32, device=gdev)
+                       for _ in range(NB)] if rank == 0 and i16 else None
 
         def disp_view(buf):  # [hb, W] disparity plane of a packed buffer (or [world, hb, W])
             d = buf[..., :dbytes].view(torch.int16 if i16 else
@@ -363,7 +423,7 @@ def main():
             pending[i].wait()
             pending[i] = None
             if rank == 0 and i16:
-                frame_disp.copy_(disp_view(recv_all[i]))
+                frame_disps[i].copy_(disp_view(recv_all[i]))
     state = {"k": 0}
 
     def step():
@@ -378,7 +438,7 @@ def main():
             if pending[i] is not None:
                 land(i)  # this stream waits for the gather that last read sends[i]
             buf = sends[i]
-            if args.backend == "nccl":
+            if nccl:
                 engines[f].match(s0, s1, mcfg, out=disp_view(buf)[:rows],
                                  corrmap=corr_view(buf)[:rows] if has_corr else None)
             else:
@@ -424,32 +484,23 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64,
-                         device=dev if args.backend == "nccl" else "cpu")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if nccl else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    if gather and args.verify_gather and rank == 0:
-        # every gather has landed (drain): slot (K-1) % NB holds the last step's frame
-        last = (state["k"] - 1) % NB
-        FL, FR = stereo_stack(n, H, W, np.uint8, row_begin=0, row_end=H)
-        fd, fc = eng.match(torch.from_numpy(FL).to(dev), torch.from_numpy(FR).to(dev), mcfg)
-        fd = fd.float().cpu() if not has_corr else fd.cpu()
-        got_d = (frame_disp if i16 else disp_view(recv_all[last])).float().cpu()
-        for r in range(world):
-            rb, re_ = band_rows(H, world, r)
-            if not torch.equal(got_d[r, :re_ - rb].view(torch.int32) if has_corr else
-                               got_d[r, :re_ - rb], fd[rb:re_].view(torch.int32) if has_corr
-                               else fd[rb:re_]):
-                raise SystemExit("verify-gather: disparity band %d differs" % r)
-            if has_corr and not torch.equal(
-                    corr_view(recv_all[last])[r, :re_ - rb].cpu().view(torch.int32),
-                    fc[rb:re_].cpu().view(torch.int32)):
-                raise SystemExit("verify-gather: corrmap band %d differs" % r)
-        print("verify-gather: %d bands byte-identical to the whole-frame match" % world,
-              file=sys.stderr)
+    # ---- after the timed region: the gather alone, then the gathered frames verified
+    gather_info = None
+    verify = None
+    if gather:
+        gather_info = time_gather(dist, torch, dev, nccl, rank, sends[0], recvs[0], nbytes, world)
+        if not args.no_verify_gather:
+            verify = verify_gather(args, C, dist, torch, np, dev, nccl, rank, world, eng, mcfg,
+                                   step, drain, NB, recv_all, frame_disps, disp_view, corr_view,
+                                   i16, has_corr)
 
-    frames_px = H * W * (world if args.scaling == "weak" else 1)
+    # pixels of one step over the whole job: the frame (strong scaling), a frame per rank
+    # (weak), or the band itself (--band-of profiling)
+    frames_px = rows * W if args.band_of > 1 else H * W * (world if args.scaling == "weak" else 1)
     value = frames_px * args.steps / elapsed / 1e6
     ms_per_step = elapsed / args.steps * 1e3
 
@@ -465,176 +516,37 @@ def main():
         serial.append((time.perf_counter() - t1) / 10 * 1e3)
     ms_serial = sorted(serial)[1]
 
-    # ---- dominant kernel, timed live: HIP events on the stream the search runs on
-    st = torch.cuda.current_stream(dev)
-    d0 = eng.transform(s0, mcfg.mode, words)
-    d1 = eng.transform(s1, mcfg.mode, words)
-    raw = torch.empty((rows, W), dtype=torch.int16, device=dev)
-    flags = (2 | (1 if mcfg.no_dupes else 0)) if mcfg.variant == 1 else 1
-    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
-    # the pipeline fuses the NXC agree into the search epilogue when there is no
-    # Consistency / subpixel / DOUBLE (engine.cpp match_device): time that launch then
-    mc = C["cfg"]
-    # (engine.cpp match_device: with the VALU search unless BICOS_FUSE_AGREE=0; with the
-    # matrix-core search only when BICOS_FUSE_AGREE=1)
-    fuse_env = os.environ.get("BICOS_FUSE_AGREE", "")
-    fused_agree = (mcfg.variant == 0 and mcfg.nxcorr_threshold is not None and
-                   not mc.get("subpixel_step") and not mcfg.precision and
-                   (fuse_env == "1" if mx_search() else fuse_env != "0"))
-    mv = mc.get("min_variance")
-    mv = None if mv is None or mv < 0 else mv * n
+    # (--kernel-reps 0: no back-to-back kernel loops -- the PMC passes use it, so every
+    # dispatch they count is an in-frame one)
+    roof = kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, world,
+                           ms_per_step, frames_px) if args.kernel_reps > 0 else None
 
-    def search_launch():
-        if fused_agree:
-            eng.search_agree(d0, d1, s0, s1, words, mcfg.nxcorr_threshold, minvar_scaled=mv)
-        else:
-            # with the used-bits hint the pipeline passes (engine.cpp match_device)
-            eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw, bits=ubits)
-
-    ubits = device.used_bits(n, mcfg.mode)
-    search_launch()  # warm
-    ev[0].record(st)
-    for _ in range(args.kernel_reps):
-        search_launch()
-    ev[1].record(st)
-    for _ in range(args.kernel_reps):
-        eng.transform(s0, mcfg.mode, words, out=d0)
-    ev[2].record(st)
-    if fused_agree:  # the standalone agree below needs the int16 search result
-        eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw)
-    # the agree stage this config runs: NXC (agree_reg_kernel) or NXC + subpixel refine
-    thr = mc.get("nxcorr_threshold")
-    stage = "subpixel" if mc.get("subpixel_step") else "nxcorr"
-    if fused_agree:
-        stage = "nxcorr (standalone agree_reg_kernel; the pipeline runs it fused in the search)"
-    ev[3].record(st)
-    for _ in range(args.kernel_reps):
-        eng.agree(raw, s0, s1, 0.96 if thr is None else thr, minvar_scaled=mv,
-                  step=mc.get("subpixel_step"))
-    ev[4].record(st)
-    torch.cuda.synchronize(dev)
-    t_search = ev[0].elapsed_time(ev[1]) / args.kernel_reps * 1e-3
-    t_tf = ev[1].elapsed_time(ev[2]) / args.kernel_reps * 1e-3
-    t_agree = ev[3].elapsed_time(ev[4]) / args.kernel_reps * 1e-3
-    pairs = search_pairs(rows, W, C["cfg"])
-    achieved = pairs / t_search / 1e9
-    peak = search_pair_peak(words, C["cfg"]) / 1e9
-    # HBM stages, algorithmic bytes: transform reads n B/px and writes 4w B/px (one stack);
-    # agree reads the int16 raw disparity + 2n B per valid px, writes 8 B/px (disp + corr)
-    tf_bytes = rows * W * (n + 4 * words)
-    valid = float((raw != -32768).float().mean().item())
-    ag_bytes = rows * W * (2 + 8) + rows * W * valid * 2 * n
-    # algorithmic bytes of one search launch: both descriptor bands + the int16 output
-    search_bytes = rows * W * (2 * 4 * words + 2)
-    mx = mx_search()
-    cons = C["cfg"].get("variant", 0) == 1
-    kname = "search_mx_kernel" if mx else ("search_lr_kernel" if cons else "search16_kernel")
-    traffic = load_traffic(kname, rows, W) if args.config == "cfg2" and rows == H else None
-    if mx:
-        alg_flops, exe_flops = mx_flops(rows, W, words, C["cfg"], ubits)
-        achieved_tf = alg_flops / t_search / 1e12
-        kpeak = mx_key_pair_peak(words, C["cfg"]) / 1e9
-        evaluated = pairs * (2 if cons else 1)
-        roof = {
-            "kernel": ("search_mx_kernel<%d words> x2 (forward + reverse FP4 MFMA Hamming argmin) "
-                       "+ consistency_kernel" % words if cons else
-                       "search_mx_kernel<%d words> (FP4 MFMA Hamming products, argmin keys in the "
-                       "accumulator)%s" % (words, " + fused NXC agree epilogue" if fused_agree else "")),
-            "bound": "mfma",
-            "achieved": round(achieved_tf, 1),
-            "peak": MFMA_FP4_DENSE_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved_tf / MFMA_FP4_DENSE_TFLOPS, 4),
-            "traffic": None if traffic is None else traffic["bytes"],
-            "traffic_source": None if traffic is None else traffic["source"],
-            "algorithmic_bytes": search_bytes,
-            "algorithmic_flops": alg_flops,
-            "executed_flops": exe_flops,
-            # the K-steps the MFMA actually multiplies (256-bit descriptors of <= 192 used
-            # bits: 3 of 4) -- the same time against the executed work
-            "executed_frac": round(exe_flops / t_search / 1e12 / MFMA_FP4_DENSE_TFLOPS, 4),
-            "pairs_per_launch": evaluated,
-            "ms_per_launch": round(t_search * 1e3, 4),
-            "peak_model": "dense FP4 MFMA peak (MI355X_MICROARCH.md); algorithmic FLOPs = "
-                          "2 x descriptor bits per Hamming pair",
-            "sustained_view": {
-                "peak": MFMA_FP4_SUSTAINED_TFLOPS,
-                "frac": round(achieved_tf / MFMA_FP4_SUSTAINED_TFLOPS, 4),
-                "source": "profiles/mfma_rates_r01.jsonl (tools/mfma_rate.hip, 4 waves/SIMD)",
-            },
-            "valu_view": {
-                "what": "the VALU key reduction (v_min3 + v_xor per pair) that bounds the "
-                        "kernel; issue bound at the measured rates, see DESIGN.md s5",
-                "achieved_Gpairs": round(evaluated / t_search / 1e9, 1),
-                "peak_Gpairs": round(kpeak, 1),
-                "frac": round(evaluated / t_search / 1e9 / kpeak, 4),
-            },
-        }
-    else:
-        roof = {
-            "kernel": ("search_lr_kernel<%d words> (fused forward + reverse Hamming argmin)" % words
-                       if cons else
-                       "search16_kernel<%d words> (Hamming argmin, packed 16-bit keys)%s" %
-                       (words, " + fused NXC agree epilogue" if fused_agree else "")),
-            "bound": "valu",
-            "achieved": round(achieved, 1),
-            "peak": round(peak, 1),
-            "unit": "Gpairs/s",
-            "frac": round(achieved / peak, 4),
-            "traffic": None if traffic is None else traffic["bytes"],
-            "traffic_source": None if traffic is None else traffic["source"],
-            "algorithmic_bytes": search_bytes,
-            "pairs_per_launch": pairs,
-            "ms_per_launch": round(t_search * 1e3, 4),
-            "peak_model": "issue bound of the per-pair VALU mix at measured rates "
-                          "(full %.1f / half %.1f T lane-op/s); see DESIGN.md s5" %
-                          (VALU_FULL_TOPS, VALU_HALF_TOPS),
-            "lane_ops_view": {
-                "achieved_Tops": round(search_ops(rows, W, words, C["cfg"]) / t_search / 1e12, 2),
-                "nominal_peak_Tops": round(VALU_NOMINAL_TOPS, 1),
-                "ops_model": "one pass over the cost matrix, 32-bit keys: 2w+3 (2w+2) lane-ops per pair",
-            },
-        }
-    if stage == "subpixel":
-        # the refine is fp32-VALU work: per valid pixel and x step, n x (quadratic 5 +
-        # round/wrap 3 + mean sum 1 + centre 1 + two fma) = 12n lane-ops, plus the step's NXC
-        # (correctly rounded sqrt + division + argmax, ~30)
-        xs = subpixel_steps(mc["subpixel_step"])
-        sp_ops = rows * W * valid * xs * (12 * n + 30)
-        roof["subpixel"] = {
-            "bound": "valu (fp32)",
-            "x_steps": xs,
-            "lane_ops": sp_ops,
-            "ops_model": "per valid px and x step: 12 x n (interp 5, round/wrap 3, sum 1, "
-                         "centre 1, fma 2) + 30 (NXC sqrt/div/argmax)",
-            "achieved_Tops": round(sp_ops / t_agree / 1e12, 2),
-            "peak_Tops": VALU_FULL_TOPS,
-            "frac": round(sp_ops / t_agree / 1e12 / VALU_FULL_TOPS, 4),
-            "ms": round(t_agree * 1e3, 4),
-            "peak_source": "profiles/valu_rates_r01.jsonl (full-rate fp32/int ops, measured)",
-        }
-    roof.update({
-        "hbm": {
-            "transform_GBps": round(tf_bytes / t_tf / 1e9, 1),
-            "transform_frac": round(tf_bytes / t_tf / 1e9 / HBM_PEAK_GBS, 4),
-            "transform_ms": round(t_tf * 1e3, 4),
-            "agree_GBps": round(ag_bytes / t_agree / 1e9, 1),
-            "agree_frac": round(ag_bytes / t_agree / 1e9 / HBM_PEAK_GBS, 4),
-            "agree_ms": round(t_agree * 1e3, 4),
-            "agree_stage": stage,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-        },
-    })
-
+    # The CPU baseline runs on rank 0 after everything else (all ranks' GPU work is done);
+    # the other ranks wait on the store without spinning, so every host core is the
+    # baseline's.
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(C, args.cpu_seconds)
+    if world > 1:
+        import datetime
+        store = dist.distributed_c10d._get_default_store()
+        if rank == 0:
+            store.set("bench_cpu_baseline_done", "1")
+        else:
+            store.wait(["bench_cpu_baseline_done"], datetime.timedelta(seconds=900))
     hp = None
     if rank == 0 and world == 1 and not args.no_host_path:
         hp = host_path(C, mcfg, reps=5)
 
     if rank == 0:
+        if gather:
+            par = ("row-bands x%d + RCCL gather over xGMI" % world if nccl else
+                   "gloo rehearsal: row-bands x%d + gloo gather, ranks sharing %d GPU(s) "
+                   "(not a measurement)" % (world, ndev))
+        elif args.band_of > 1:
+            par = "single GPU, band 0 of %d (%d rows; profiling)" % (args.band_of, rows)
+        else:
+            par = "replicas x%d" % world if world > 1 else "single GPU"
         line = {
             "metric": "disparity Mpix/s + ms/match, 33x2 stack @ 2048x1536, 1/2/4/8 MI355X",
             "value": round(value, 2),
@@ -655,17 +567,331 @@ def main():
             "config": {
                 "workload": "%s: %s" % (args.config, C["desc"]),
                 "n_images": n, "rows": H, "cols": W, "descriptor_bits": 32 * words,
-                "parallelism": ("row-bands x%d + RCCL gather" % world) if gather else
-                               ("replicas x%d" % world if world > 1 else "single GPU"),
+                "rows_per_rank": rows,
+                "parallelism": par,
+                "backend": args.backend if world > 1 else None,
                 "match_config": C["cfg"],
             },
             "roofline": roof,
+            "gather": gather_info,
+            "verify_gather": verify,
             "cpu_baseline": cpu,
             "host_path": hp,
         }
+        if "published" in C:
+            pub = C["published"]
+            line["vs_published"] = dict(pub, ours_ms_per_match=round(ms_per_step, 4),
+                                        ours_ms_one_at_a_time=round(ms_serial, 4),
+                                        speedup=round(pub["ms_per_match"] / ms_per_step, 1))
         print(json.dumps(line), flush=True)
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+
+
+def time_gather(dist, torch, dev, nccl, rank, send, recv, nbytes, world, reps=10):
+    """The per-step gather alone (untimed region): median of `reps` synchronous gathers of one
+    packed band buffer to rank 0, each after a barrier. RCCL: HIP events on the current
+    stream around the collective (the RCCL stream waits for the first, the second waits for
+    the RCCL stream); gloo: host wall time."""
+    ts = []
+    for _ in range(reps):
+        dist.barrier()
+        if nccl:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            dist.gather(send, recv, dst=0)
+            e1.record()
+            torch.cuda.synchronize(dev)
+            ts.append(e0.elapsed_time(e1))
+        else:
+            t = time.perf_counter()
+            dist.gather(send, recv, dst=0)
+            ts.append((time.perf_counter() - t) * 1e3)
+    ms = sorted(ts)[len(ts) // 2]
+    to_root = (world - 1) * nbytes
+    return {"ms": round(ms, 4), "bytes_per_rank": nbytes, "bytes_to_root": to_root,
+            "GBps_into_root": round(to_root / (ms * 1e-3) / 1e9, 1),
+            "what": "median of %d synchronous gathers of the packed [disparity | corrmap] band "
+                    "buffer (%s), measured on rank %d after the timed region; inside the timed "
+                    "region the gather of step k overlaps the kernels of step k+1" %
+                    (reps, "RCCL, HIP events on the current stream" if nccl else "gloo, host "
+                     "wall time", rank)}
+
+
+def _frame_fixture(name):
+    """The oracle's whole-frame hashes for a BASELINE config (tests/golden/frames.json, data
+    written by tests/golden/make_frames.py), or None."""
+    path = os.path.join(ROOT, "tests", "golden", "frames.json")
+    try:
+        return json.load(open(path)).get(name)
+    except (OSError, ValueError):
+        return None
+
+
+def verify_gather(args, C, dist, torch, np, dev, nccl, rank, world, eng, mcfg, step, drain, NB,
+                  recv_all, frame_disps, disp_view, corr_view, i16, has_corr):
+    """Untimed: every gather slot's receive buffer (and rank 0's float frame) is overwritten
+    with a sentinel, NB more steps run with the same pipeline as the timed ones, and rank 0
+    checks every slot's gathered frame: against the oracle's whole-frame sha256 for the
+    config (tests/golden/frames.json) when it has one, else byte for byte against a one-GPU
+    match of the whole frame. A slot that did not land, landed stale or out of order keeps
+    the sentinel and fails. All ranks learn the verdict; a failure exits non-zero."""
+    import hashlib
+    from libbicos_amd.distributed import band_rows
+    from libbicos_amd.synthetic import stereo_stack
+    n, H, W = C["n"], C["H"], C["W"]
+    torch.cuda.synchronize(dev)
+    if rank == 0:
+        for i in range(NB):
+            recv_all[i].fill_(0xFF)
+            if frame_disps is not None:
+                frame_disps[i].fill_(float("nan"))
+    dist.barrier()
+    for _ in range(NB):
+        step()
+    drain()
+    torch.cuda.synchronize(dev)
+    ok, how = True, None
+    if rank == 0:
+        fx = _frame_fixture(args.config)
+        ref = None
+        if fx is None or (fx["n"], fx["H"], fx["W"]) != (n, H, W):
+            FL, FR = stereo_stack(n, H, W, np.uint8, row_begin=0, row_end=H)
+            fd, fc = eng.match(torch.from_numpy(FL).to(dev), torch.from_numpy(FR).to(dev), mcfg)
+            ref = (fd.cpu().numpy(), None if fc is None else fc.cpu().numpy())
+            how = "byte-identical to a one-GPU match of the whole frame"
+        else:
+            how = "sha256 of the whole frame == the oracle's (tests/golden/frames.json)"
+        for i in range(NB):
+            dmap = (frame_disps[i] if i16 else disp_view(recv_all[i])).cpu().numpy()
+            cmap = corr_view(recv_all[i]).cpu().numpy() if has_corr else None
+            parts_d, parts_c = [], []
+            for r in range(world):
+                rb, re_ = band_rows(H, world, r)
+                parts_d.append(dmap[r, :re_ - rb])
+                if has_corr:
+                    parts_c.append(cmap[r, :re_ - rb])
+            fd_ = np.ascontiguousarray(np.concatenate(parts_d))
+            fc_ = np.ascontiguousarray(np.concatenate(parts_c)) if has_corr else None
+            if ref is None:
+                sha = lambda a: hashlib.sha256(a.tobytes()).hexdigest()  # noqa: E731
+                good = sha(fd_) == fx["disparity_sha256"] and (
+                    not has_corr or sha(fc_) == fx["corrmap_sha256"])
+            else:
+                good = fd_.tobytes() == ref[0].tobytes() and (
+                    not has_corr or fc_.tobytes() == ref[1].tobytes())
+            if not good:
+                ok = False
+                how = "slot %d of %d: gathered frame differs (%s)" % (i, NB, how)
+                break
+    flag = torch.tensor([1.0 if ok else 0.0], device=dev if nccl else "cpu")
+    dist.broadcast(flag, src=0)
+    if flag.item() != 1.0:
+        raise SystemExit("verify-gather failed: %s" % (how or "see rank 0"))
+    if rank == 0:
+        print("verify-gather: %d slots x %d bands, %s" % (NB, world, how), file=sys.stderr)
+    return {"ok": True, "slots": NB, "bands": world, "check": how}
+
+
+def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, world,
+                    ms_per_step, step_px):
+    """The dominant kernel (the Hamming search) and the HBM-bound stages, each launched
+    back to back on this rank's band and timed with HIP events on the stream they run on,
+    against their rooflines; PMC HBM bytes from profiles/ when they were
+    measured on these sources; the whole match's HBM-read fraction."""
+    st = torch.cuda.current_stream(dev)
+    d0 = eng.transform(s0, mcfg.mode, words)
+    d1 = eng.transform(s1, mcfg.mode, words)
+    raw = torch.empty((rows, W), dtype=torch.int16, device=dev)
+    flags = (2 | (1 if mcfg.no_dupes else 0)) if mcfg.variant == 1 else 1
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
+    mc = C["cfg"]
+    # the pipeline fuses the NXC agree into the search epilogue (engine.cpp match_device)
+    # only with the VALU search (BICOS_SEARCH=valu) unless BICOS_FUSE_AGREE=0
+    fuse_env = os.environ.get("BICOS_FUSE_AGREE", "")
+    fused_agree = (mcfg.variant == 0 and mcfg.nxcorr_threshold is not None and
+                   not mc.get("subpixel_step") and not mcfg.precision and
+                   (fuse_env == "1" if mx_search() else fuse_env != "0"))
+    mv = mc.get("min_variance")
+    mv = None if mv is None or mv < 0 else mv * n
+    from libbicos_amd import device
+    ubits = device.used_bits(n, mcfg.mode)
+    sbits = transform_bits(n, mcfg.mode)
+
+    def search_launch():
+        if fused_agree:
+            eng.search_agree(d0, d1, s0, s1, words, mcfg.nxcorr_threshold, minvar_scaled=mv)
+        else:
+            # with the used-bits hint the pipeline passes (engine.cpp match_device)
+            eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw, bits=ubits)
+
+    reps = args.kernel_reps
+    search_launch()  # warm
+    ev[0].record(st)
+    for _ in range(reps):
+        search_launch()
+    ev[1].record(st)
+    for _ in range(reps):
+        eng.transform(s0, mcfg.mode, words, out=d0)
+    ev[2].record(st)
+    if fused_agree:  # the standalone agree below needs the int16 search result
+        eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw)
+    thr = mc.get("nxcorr_threshold")
+    stage = "subpixel" if mc.get("subpixel_step") else "nxcorr"
+    if fused_agree:
+        stage = "nxcorr (standalone agree kernel; the pipeline runs it fused in the search)"
+    ev[3].record(st)
+    for _ in range(reps):
+        eng.agree(raw, s0, s1, 0.96 if thr is None else thr, minvar_scaled=mv,
+                  step=mc.get("subpixel_step"))
+    ev[4].record(st)
+    torch.cuda.synchronize(dev)
+    t_search = ev[0].elapsed_time(ev[1]) / reps * 1e-3
+    t_tf = ev[1].elapsed_time(ev[2]) / reps * 1e-3
+    t_agree = ev[3].elapsed_time(ev[4]) / reps * 1e-3
+    pairs = search_pairs(rows, W, mc)
+    # HBM stages, algorithmic bytes: transform reads n B/px and writes 4w B/px (one stack);
+    # agree reads the int16 raw disparity + 2n B per valid px, writes 8 B/px (disp + corr)
+    tf_bytes = rows * W * (n + 4 * words)
+    valid = float((raw != -32768).float().mean().item())
+    ag_bytes = rows * W * (2 + 8) + rows * W * valid * 2 * n
+    # algorithmic bytes of one search launch: both descriptor bands + the int16 output
+    search_bytes = rows * W * (2 * 4 * words + 2)
+    mx = mx_search()
+    cons = mc.get("variant", 0) == 1
+    kname = "search_mx_kernel" if mx else ("search_lr_kernel" if cons else "search16_kernel")
+    cfgname = args.config
+    traffic = load_traffic(kname, cfgname, rows)
+    if mx:
+        alg_flops, used_flops = mx_flops(rows, W, words, mc, ubits, sbits)
+        achieved_tf = alg_flops / t_search / 1e12
+        kpeak = mx_key_pair_peak(words, mc) / 1e9
+        evaluated = pairs * (2 if cons else 1)
+        k_exec = int(round(alg_flops / (2 * evaluated)))
+        roof = {
+            "kernel": ("search_mx_kernel<%d words> x2 (forward + reverse FP4 MFMA Hamming argmin) "
+                       "+ consistency_kernel" % words if cons else
+                       "search_mx_kernel<%d words> (FP4 MFMA Hamming products, argmin keys in the "
+                       "accumulator)%s" % (words, " + fused NXC agree epilogue" if fused_agree else "")),
+            "bound": "mfma",
+            "achieved": round(achieved_tf, 1),
+            "peak": MFMA_FP4_DENSE_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": round(achieved_tf / MFMA_FP4_DENSE_TFLOPS, 4),
+            "traffic": traffic["bytes"],
+            "traffic_source": traffic.get("source") or traffic.get("why"),
+            "algorithmic_bytes": search_bytes,
+            "algorithmic_flops": alg_flops,
+            "k_bits_per_pair": k_exec,
+            "used_bits_view": {
+                "what": "the same launch time against 2 x the bits the transform sets per "
+                        "descriptor (%d of %d)" % (sbits, k_exec),
+                "flops": used_flops,
+                "frac": round(used_flops / t_search / 1e12 / MFMA_FP4_DENSE_TFLOPS, 4),
+            },
+            "pairs_per_launch": evaluated,
+            "ms_per_launch": round(t_search * 1e3, 4),
+            "peak_model": "dense FP4 MFMA peak (MI355X_MICROARCH.md); algorithmic FLOPs = 2 x K "
+                          "per Hamming pair, K = the descriptor bits multiplied (the descriptor "
+                          "width, less whole 64-bit K-steps above the set bits): never more "
+                          "than executed",
+            "sustained_view": {
+                "peak": MFMA_FP4_SUSTAINED_TFLOPS,
+                "frac": round(achieved_tf / MFMA_FP4_SUSTAINED_TFLOPS, 4),
+                "source": "profiles/mfma_rates_r01.jsonl (tools/mfma_rate.hip, 4 waves/SIMD)",
+            },
+            "valu_view": {
+                "what": "the VALU key reduction (v_min3 + v_xor per pair) that bounds the "
+                        "kernel; issue bound at the measured rates, see DESIGN.md s5",
+                "achieved_Gpairs": round(evaluated / t_search / 1e9, 1),
+                "peak_Gpairs": round(kpeak, 1),
+                "frac": round(evaluated / t_search / 1e9 / kpeak, 4),
+            },
+        }
+    else:
+        achieved = pairs / t_search / 1e9
+        peak = search_pair_peak(words, mc) / 1e9
+        roof = {
+            "kernel": ("search_lr_kernel<%d words> (fused forward + reverse Hamming argmin)" % words
+                       if cons else
+                       "search16_kernel<%d words> (Hamming argmin, packed 16-bit keys)%s" %
+                       (words, " + fused NXC agree epilogue" if fused_agree else "")),
+            "bound": "valu",
+            "achieved": round(achieved, 1),
+            "peak": round(peak, 1),
+            "unit": "Gpairs/s",
+            "frac": round(achieved / peak, 4),
+            "traffic": traffic["bytes"],
+            "traffic_source": traffic.get("source") or traffic.get("why"),
+            "algorithmic_bytes": search_bytes,
+            "pairs_per_launch": pairs,
+            "ms_per_launch": round(t_search * 1e3, 4),
+            "peak_model": "issue bound of the per-pair VALU mix at measured rates "
+                          "(full %.1f / half %.1f T lane-op/s); see DESIGN.md s5" %
+                          (VALU_FULL_TOPS, VALU_HALF_TOPS),
+            "lane_ops_view": {
+                "achieved_Tops": round(search_ops(rows, W, words, mc) / t_search / 1e12, 2),
+                "nominal_peak_Tops": round(VALU_NOMINAL_TOPS, 1),
+                "ops_model": "one pass over the cost matrix, 32-bit keys: 2w+3 (2w+2) lane-ops per pair",
+            },
+        }
+    if stage == "subpixel":
+        # the refine is fp32-VALU work: per valid pixel and x step, n x (quadratic 5 +
+        # round/wrap 3 + mean sum 1 + centre 1 + two fma) = 12n lane-ops, plus the step's NXC
+        # (correctly rounded sqrt + division + argmax, ~30)
+        xs = subpixel_steps(mc["subpixel_step"])
+        sp_ops = rows * W * valid * xs * (12 * n + 30)
+        ach = sp_ops / t_agree / 1e12
+        roof["subpixel"] = {
+            "bound": "valu (fp32)",
+            "x_steps": xs,
+            "lane_ops": sp_ops,
+            "ops_model": "per valid px and x step: 12 x n (interp 5, round/wrap 3, sum 1, "
+                         "centre 1, fma 2) + 30 (NXC sqrt/div/argmax)",
+            "achieved_Tops": round(ach, 2),
+            "peak_Tops": round(VALU_NOMINAL_TOPS, 1),
+            "frac": round(ach / VALU_NOMINAL_TOPS, 4),
+            "peak_source": "spec: 256 CUs x 128 fp32 lanes/clk x 2.4 GHz = 78.6 T lane-op/s "
+                           "(MI355X_MICROARCH.md 157.3 TF fp32 / 2)",
+            "measured_view": {"peak_Tops": VALU_FULL_TOPS,
+                              "frac": round(ach / VALU_FULL_TOPS, 4),
+                              "source": "profiles/valu_rates_r01.jsonl (full-rate ops at the "
+                                        "held clock, measured)"},
+            "ms": round(t_agree * 1e3, 4),
+        }
+    tf_tr = load_traffic("transform", cfgname, rows)
+    ag_tr = load_traffic("subpixel" if stage == "subpixel" else "agree", cfgname, rows)
+    roof["hbm"] = {
+        "transform_GBps": round(tf_bytes / t_tf / 1e9, 1),
+        "transform_frac": round(tf_bytes / t_tf / 1e9 / HBM_PEAK_GBS, 4),
+        "transform_ms": round(t_tf * 1e3, 4),
+        "transform_traffic": tf_tr["bytes"] and tf_tr["bytes"] / 2,  # PMC: both stacks / 2
+        "agree_GBps": round(ag_bytes / t_agree / 1e9, 1),
+        "agree_frac": round(ag_bytes / t_agree / 1e9 / HBM_PEAK_GBS, 4),
+        "agree_ms": round(t_agree * 1e3, 4),
+        "agree_traffic": ag_tr["bytes"],
+        "agree_stage": stage,
+        "traffic_source": tf_tr.get("source") or tf_tr.get("why"),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+    }
+    # the whole match against the HBM-read roofline (the north star's unit): the bytes each
+    # stage must read from HBM per frame -- both stacks (transform), both descriptor sets
+    # (search), raw disparity + the samples of valid pixels (agree) -- over the whole job's
+    # time per frame, against N x 8 TB/s
+    P = step_px
+    read_bytes = 2 * n * P + 2 * 4 * words * P + 2 * P + valid * 2 * n * P
+    roof["match_hbm_read"] = {
+        "bytes_per_frame": int(read_bytes),
+        "achieved_GBps": round(read_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+        "peak_GBps": HBM_PEAK_GBS * world,
+        "frac": round(read_bytes / (ms_per_step * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4),
+        "model": "transform 2nP + search 2*4wP + agree (2P + valid*2nP) bytes read per frame, "
+                 "P = %d px, over ms_per_step, vs %d x 8 TB/s" % (P, world),
+    }
+    return roof
 
 
 def host_path(C, mcfg, reps):

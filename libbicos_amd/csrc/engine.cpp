@@ -125,9 +125,10 @@ bool use_mx(const bicos_engine* e) {
 }
 
 // Highest descriptor bit the transform writes + 1 (an upper bound: LIMITED writes 4n-6 bits
-// for n >= 4, FULL n^2-2n+3; descriptor_transform.hpp:31-123). The search multiplies only
-// the 64-bit K-steps that hold them.
-int used_bits(int n, int mode) { return mode ? n * n - 2 * n + 3 : 4 * n - 5; }
+// for n >= 4, 7 for n = 3 and 4 for n = 2 -- the closing four comparisons alone,
+// descriptor_transform.hpp:62-68 --, FULL n^2-2n+3; descriptor_transform.hpp:31-123). The
+// search multiplies only the 64-bit K-steps that hold them.
+int used_bits(int n, int mode) { return mode ? n * n - 2 * n + 3 : std::max(4 * n - 5, 4); }
 
 bicos_hip::MxGeometry mx_geometry(const bicos_engine* e, int rows, int cols, int words,
                                   int bits = 0) {

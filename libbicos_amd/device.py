@@ -246,9 +246,10 @@ class Engine:
 
 
 def used_bits(n: int, mode: int = 0) -> int:
-    """Upper bound of the descriptor bits the transform sets (LIMITED 4n-6 for n >= 4,
-    FULL n^2-2n+3; reference descriptor_transform.hpp:31-123)."""
-    return n * n - 2 * n + 3 if mode else 4 * n - 5
+    """Upper bound of the descriptor bits the transform sets (LIMITED 4n-6 for n >= 4, 7 for
+    n = 3, 4 for n = 2 (descriptor_transform.hpp:62-68 alone); FULL n^2-2n+3; reference
+    descriptor_transform.hpp:31-123)."""
+    return n * n - 2 * n + 3 if mode else max(4 * n - 5, 4)
 
 
 def descriptor_words(n: int, mode: int = 0) -> int:

@@ -42,3 +42,31 @@ def test_failing_rank_fails_the_launch():
     p = _run(["--gpus", "2", "--backend", "gloo", "--selftest-launch"],
              {"BICOS_SELFTEST_FAIL_RANK": "1"})
     assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
+
+
+@pytest.mark.gpu
+def test_two_rank_gloo_line_has_every_field():
+    """The N>1 bench line is self-contained: two gloo ranks sharing the
+    box's GPU run the row-band path; rank 0's line carries the CPU baseline, the search
+    roofline with its PMC traffic lookup, the gather timed on its own, the gathered frames
+    verified against the oracle's whole-frame hash, and a "gloo rehearsal" label."""
+    p = _run(["--gpus", "2", "--backend", "gloo", "--steps", "3", "--warmup", "1",
+              "--cpu-seconds", "2", "--kernel-reps", "2", "--no-host-path"], timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0
+    assert "gloo rehearsal" in d["config"]["parallelism"]
+    assert d["config"]["rows_per_rank"] == 768
+    cpu = d["cpu_baseline"]
+    assert cpu and cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port"
+    roof = d["roofline"]
+    assert roof["bound"] == "mfma" and 0 < roof["frac"] < 1
+    assert "traffic" in roof and roof["traffic_source"]
+    assert roof["match_hbm_read"]["peak_GBps"] == 16000.0
+    g = d["gather"]
+    assert g["ms"] > 0 and g["bytes_to_root"] == g["bytes_per_rank"]
+    v = d["verify_gather"]
+    assert v["ok"] and v["slots"] >= 2 and v["bands"] == 2
+    assert "frames.json" in v["check"]

@@ -33,13 +33,25 @@ def test_mx_ksteps(words, bits, ks):
 
 
 def test_mx_flops_cfg2_and_cfg4():
+    """Algorithmic K never exceeds the executed K-steps (cfg4 was priced
+    on 256 padded bits); the used-bit view prices the bits the transform sets."""
     cfg2 = bench.CONFIGS["cfg2"]
-    alg, exe = bench.mx_flops(1536, 2048, 4, cfg2["cfg"], 4 * 33 - 5)
-    assert alg == exe == 1536 * 2048 * 2048 * 2 * 128
+    alg, used = bench.mx_flops(1536, 2048, 4, cfg2["cfg"], 4 * 33 - 5, bench.transform_bits(33, 0))
+    assert alg == 1536 * 2048 * 2048 * 2 * 128
+    assert used == 1536 * 2048 * 2048 * 2 * 126
     cfg4 = bench.CONFIGS["cfg4"]
-    alg, exe = bench.mx_flops(1536, 2048, 8, cfg4["cfg"], 4 * 40 - 5)
+    alg, used = bench.mx_flops(1536, 2048, 8, cfg4["cfg"], 4 * 40 - 5, bench.transform_bits(40, 0))
     pairs = 2 * 1536 * 2048 * 2048  # forward + reverse
-    assert alg == pairs * 2 * 256 and exe == pairs * 2 * 192
+    assert alg == pairs * 2 * 192 and used == pairs * 2 * 154
+
+
+def test_transform_bits_match_the_oracle(oracle):
+    from libbicos_amd.synthetic import random_stack
+    for n, mode in [(2, 0), (3, 0), (4, 0), (33, 0), (40, 0), (5, 1), (16, 1)]:
+        d = oracle.transform(random_stack(n, 32, 64, seed=n), mode, 8)
+        hi = max(32 * w + int(np.floor(np.log2(d[..., w][d[..., w] != 0].astype(np.float64)).max()))
+                 for w in range(8) if (d[..., w] != 0).any())
+        assert hi + 1 == bench.transform_bits(n, mode), (n, mode)
 
 
 def test_configs_match_the_baseline():

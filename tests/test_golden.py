@@ -55,3 +55,30 @@ def test_gpu_reproduces_golden(gpu, golden, case):
         assert _same(d.cpu().numpy(), golden["%s/%s/disparity" % (name, cname)]), (name, cname)
         if corr is not None:
             assert _same(corr.cpu().numpy(), golden["%s/%s/corrmap" % (name, cname)]), (name, cname)
+
+
+# ------------------------------------------ whole-frame fixtures (tests/golden/frames.json)
+def _frames():
+    import json
+    return json.load(open(os.path.join(os.path.dirname(GOLDEN), "frames.json")))
+
+
+def test_frames_cover_every_config():
+    from tests.golden.make_frames import FRAMES
+    db = _frames()
+    assert sorted(db) == sorted(FRAMES)
+    for name, (n, H, W, cfg) in FRAMES.items():
+        r = db[name]
+        assert (r["n"], r["H"], r["W"], r["config"]) == (n, H, W, cfg), name
+        assert len(r["disparity_bands"]) == -(-H // r["band_rows"])
+
+
+def test_oracle_reproduces_frame_cfg1(oracle):
+    """The cheapest whole frame (BASELINE cfg1) regenerates from the committed generator +
+    oracle to the same hashes (the others take minutes; make_frames.py rebuilds them)."""
+    from libbicos_amd.synthetic import stereo_stack
+    from tests.golden.make_frames import frame_record
+    rec = _frames()["cfg1"]
+    L, R = stereo_stack(rec["n"], rec["H"], rec["W"])
+    d, c = oracle.match(L, R, oracle.OracleConfig(**rec["config"]))
+    assert frame_record(rec["n"], rec["H"], rec["W"], rec["config"], L, R, d, c) == rec

@@ -255,42 +255,103 @@ def test_pybicos_consistency_and_subpixel(gpu, oracle):
 
 
 # ------------------------------------------------- full size (BASELINE shapes)
-def _full_size_check(gpu, oracle, n, H, W, cfg, rows):
-    L, R = stereo_stack(n, H, W)
+# Whole frames against tests/golden/frames.json (tests/golden/make_frames.py): the C oracle's
+# sha256 of the full disparity map and corrmap of every BASELINE config and the reference
+# README's full-match shape. Every pixel is compared; a mismatch names its 64-row bands and
+# the oracle is re-run on the first bad band for the message.
+_FRAMES = None
+_STACKS = {}
+
+
+def _frames():
+    global _FRAMES
+    if _FRAMES is None:
+        import json
+        import os
+        _FRAMES = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "frames.json")))
+    return _FRAMES
+
+
+def _frame_stacks(n, H, W):
+    key = (n, H, W)
+    if key not in _STACKS:
+        _STACKS.clear()  # one frame's stacks at a time (cfg5: 0.55 GB of host memory)
+        _STACKS[key] = stereo_stack(n, H, W)
+    return _STACKS[key]
+
+
+def _check_frame(gpu, oracle, name):
+    from tests.golden.make_frames import band_hashes, sha
+    rec = _frames()[name]
+    n, H, W, cfg = rec["n"], rec["H"], rec["W"], rec["config"]
+    L, R = _frame_stacks(n, H, W)
+    assert [sha(L), sha(R)] == rec["inputs_sha256"], "synthetic generator changed"
     got_d, got_c = gpu_match(gpu, L, R, **cfg)
-    # rows are independent: the oracle on a band of rows equals those rows of the frame
-    for (b, e) in rows:
-        rd, rc = oracle.match(L[:, b:e], R[:, b:e], oracle.OracleConfig(**cfg))
-        same(got_d[b:e].copy(), rd)
-        if rc is not None:
-            same(got_c[b:e].copy(), rc)
+    assert str(got_d.dtype) == rec["disparity_dtype"]
+    maps = [("disparity", got_d)] + ([("corrmap", got_c)] if rec["corrmap_sha256"] else [])
+    for what, m in maps:
+        if sha(m) == rec[what + "_sha256"]:
+            continue
+        bad = [i for i, (a, b) in enumerate(zip(band_hashes(m, rec["band_rows"]),
+                                                rec[what + "_bands"])) if a != b]
+        b0 = bad[0] * rec["band_rows"]
+        e0 = min(H, b0 + rec["band_rows"])
+        rd, rc = oracle.match(L[:, b0:e0], R[:, b0:e0], oracle.OracleConfig(**cfg))
+        try:
+            same(m[b0:e0].copy(), rd if what == "disparity" else rc)
+        except AssertionError as ex:
+            raise AssertionError("%s %s: %d of %d bands differ; rows %d-%d: %s" % (
+                name, what, len(bad), len(rec[what + "_bands"]), b0, e0, ex))
+        raise AssertionError("%s %s: %d bands differ, yet rows %d-%d match the oracle" % (
+            name, what, len(bad), b0, e0))
+    return got_d, got_c
+
+
+def _planted(got_d, H):
     truth = (16 + (48 * np.arange(H)) // H)[:, None]
     d = got_d.astype(np.float64)
     valid = np.isfinite(d) & (d != -32768)
     return valid, np.abs(d - truth)
 
 
-def test_cfg2_full_size(gpu, oracle):
-    """2048x1536x33 LIMITED (128-bit), thr 0.96: oracle-checked bands + planted truth."""
-    valid, err = _full_size_check(gpu, oracle, 33, 1536, 2048, dict(nxcorr_threshold=0.96),
-                                  [(0, 8), (760, 768), (1528, 1536)])
+def test_full_frame_cfg1(gpu, oracle):
+    """BASELINE cfg1 (8 images, 640x480, nxcorr 0.9): the whole frame."""
+    _check_frame(gpu, oracle, "cfg1")
+
+
+def test_full_frame_cfg2(gpu, oracle):
+    """2048x1536x33 LIMITED (128-bit), thr 0.96: every pixel vs the oracle + planted truth."""
+    got_d, _ = _check_frame(gpu, oracle, "cfg2")
+    valid, err = _planted(got_d, 1536)
     assert valid.mean() > 0.95
     assert (err[valid] == 0).mean() > 0.99
 
 
-def test_cfg3_full_size(gpu, oracle):
-    valid, err = _full_size_check(gpu, oracle, 33, 1536, 2048,
-                                  dict(nxcorr_threshold=0.96, min_variance=2.0, subpixel_step=0.1),
-                                  [(100, 104), (1200, 1204)])
+def test_full_frame_cfg2_search(gpu, oracle):
+    """cfg2 without the NXC stage: the int16 NoDuplicates search result, every pixel."""
+    _check_frame(gpu, oracle, "cfg2_raw")
+
+
+def test_full_frame_cfg3(gpu, oracle):
+    got_d, _ = _check_frame(gpu, oracle, "cfg3")
+    valid, err = _planted(got_d, 1536)
     assert valid.mean() > 0.9
     assert (err[valid] <= 1.0).all()
 
 
-def test_cfg4_full_size(gpu, oracle):
-    valid, err = _full_size_check(gpu, oracle, 40, 1536, 2048,
-                                  dict(nxcorr_threshold=0.96, variant=1, max_lr_diff=1),
-                                  [(0, 4), (1000, 1004)])
+def test_full_frame_cfg4(gpu, oracle):
+    got_d, _ = _check_frame(gpu, oracle, "cfg4")
+    valid, _ = _planted(got_d, 1536)
     assert valid.mean() > 0.9
+
+
+def test_full_frame_readme(gpu, oracle):
+    """The reference README's published full match (README.md:80,90): 3208x2200 x33,
+    --limited --threshold 0.96 --variance 2.0 --step 0.1."""
+    got_d, _ = _check_frame(gpu, oracle, "readme")
+    valid, err = _planted(got_d, 2200)
+    assert valid.mean() > 0.9
+    assert (err[valid] <= 1.0).all()
 
 
 def test_row_band_sharding_is_exact(gpu):
@@ -613,22 +674,16 @@ def test_mx_is_the_default_search(gpu):
 
 # ---------------------------------------------- cfg5: 4K frame, 8 row bands of 270
 def test_cfg5_full_size_and_bands(gpu, oracle):
-    """3840x2160x33 (BASELINE cfg5) on one GPU: oracle-checked rows of the whole-frame
-    match, and the 8 row bands of 270 the 8-GPU run computes are byte-identical to it."""
-    import torch
+    """3840x2160x33 (BASELINE cfg5) on one GPU: the whole frame against the oracle's hashes
+    (tests/golden/frames.json), and the 8 row bands of 270 the 8-GPU run computes are
+    byte-identical to it."""
     from libbicos_amd.device import MatchConfig
     from libbicos_amd.distributed import band_rows
     n, H, W = 33, 2160, 3840
     cfg = dict(nxcorr_threshold=0.96)
-    L, R = stereo_stack(n, H, W)
+    got_d, got_c = _check_frame(gpu, oracle, "cfg5")
+    L, R = _frame_stacks(n, H, W)
     s0, s1 = dev(L), dev(R)
-    full_d, full_c = gpu.match(s0, s1, MatchConfig(**cfg))
-    torch.cuda.synchronize()
-    got_d, got_c = host(full_d), host(full_c)
-    for (b, e) in [(0, 2), (1079, 1081), (2158, 2160)]:
-        rd, rc = oracle.match(L[:, b:e], R[:, b:e], oracle.OracleConfig(**cfg))
-        same(got_d[b:e].copy(), rd)
-        same(got_c[b:e].copy(), rc)
     for r in range(8):
         b, e = band_rows(H, 8, r)
         assert e - b == 270

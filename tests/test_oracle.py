@@ -50,6 +50,23 @@ def test_limited_uses_4n_minus_6_bits(oracle, n):
     assert top == 4 * n - 7
 
 
+@pytest.mark.parametrize("mode", [0, 1])
+def test_used_bits_bounds_every_set_bit(oracle, mode):
+    """device.used_bits (the search's K-step hint, engine.cpp used_bits) is an upper bound of
+    the highest descriptor bit the transform sets, for every n of both modes (ADVICE r02:
+    LIMITED n = 2 sets 4 bits, descriptor_transform.hpp:62-68)."""
+    from libbicos_amd.device import used_bits
+    for n in range(2, 66 if mode == 0 else 17):
+        s = random_stack(n, 16, 64, seed=1000 + n)
+        d = oracle.transform(s, mode, 8)
+        hi = -1
+        for w in range(8):
+            nz = d[..., w] != 0
+            if nz.any():
+                hi = 32 * w + int(np.max(np.floor(np.log2(d[..., w][nz].astype(np.float64)))))
+        assert hi < used_bits(n, mode), (n, mode, hi)
+
+
 @pytest.mark.parametrize("n", [2, 3, 4, 8, 10, 16])
 def test_full_bit_count(oracle, n):
     s = random_stack(n, 64, 64, seed=100 + n)

@@ -132,6 +132,26 @@ for step in "$@"; do
                 run abpipe_alt$k 300 python tools/frame_pipe_bench.py --ns 1,8 --streams 1,3 --rounds 2
             done
             cp build/cur.so libbicos_amd/libbicos_amd.so ;;
+        pmchead)  # HBM bytes per in-frame dispatch at HEAD: FETCH_SIZE and WRITE_SIZE passes per
+                  # config / band (PMCSETS="cfg2:1 cfg2:8 ..."), summarised by tools/pmc_summary.py
+            mkdir -p gpurun_out/pmc
+            python -c "import bench; print(bench.kernel_source_hash())" > gpurun_out/pmc/source_sha
+            for cb in ${PMCSETS:-cfg2:1 cfg2:2 cfg2:4 cfg2:8 cfg3:1 cfg4:1 cfg5:1 cfg5:8 readme:1 cfg1:1}; do
+                c=${cb%%:*}; nb=${cb##*:}
+                for set in FETCH_SIZE WRITE_SIZE; do
+                    run pmc_${c}_b${nb}_${set} 150 timeout -s KILL 140 rocprofv3 --pmc $set -d gpurun_out/pmc/${c}__b${nb}__${set} -o run --output-format csv -- python bench.py --config $c --band-of $nb --steps 3 --warmup 1 --spinup-ms 0 --kernel-reps 0 --inflight 1 --no-cpu-baseline --no-host-path
+                done
+            done ;;
+        pmcstall)  # stall / occupancy / memory-latency counters of the in-frame kernels (PMCSETS as above)
+            mkdir -p gpurun_out/pmc
+            python -c "import bench; print(bench.kernel_source_hash())" > gpurun_out/pmc/source_sha
+            for cb in ${PMCSETS:-cfg2:1}; do
+                c=${cb%%:*}; nb=${cb##*:}
+                run pmc_${c}_b${nb}_sq 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU GRBM_GUI_ACTIVE TA_TA_BUSY_sum TD_TD_BUSY_sum -d gpurun_out/pmc/${c}__b${nb}__sq -o run --output-format csv -- python bench.py --config $c --band-of $nb --steps 3 --warmup 1 --spinup-ms 0 --kernel-reps 0 --inflight 1 --no-cpu-baseline --no-host-path
+                run pmc_${c}_b${nb}_mem 150 timeout -s KILL 140 rocprofv3 --pmc TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCC_HIT_sum TCC_MISS_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TD_TC_STALL_sum TD_SPI_STALL_sum GRBM_GUI_ACTIVE SQ_WAVES -d gpurun_out/pmc/${c}__b${nb}__mem -o run --output-format csv -- python bench.py --config $c --band-of $nb --steps 3 --warmup 1 --spinup-ms 0 --kernel-reps 0 --inflight 1 --no-cpu-baseline --no-host-path
+            done ;;
+        benchg2)  # the N=2 path rehearsed with gloo ranks sharing the one GPU (all line fields)
+            run benchg2 600 python bench.py --gpus 2 --backend gloo --steps 5 --warmup 1 --cpu-seconds 4 ;;
         *) echo "unknown step $step" ;;
     esac
 done
