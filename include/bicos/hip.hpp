@@ -6,11 +6,10 @@
 // same arguments (Image for cv::Mat / cv::cuda::GpuMat, hipStream_t for cv::cuda::Stream).
 #pragma once
 
-#include <hip/hip_runtime_api.h>
 
 #include <vector>
 
-#include "common.hpp"
+#include "types.hpp"
 
 namespace BICOS::impl::hip {
 
@@ -19,7 +18,7 @@ namespace BICOS::impl::hip {
 // (synchronous). Device images: zero-copy when each stack is one planar buffer (equal
 // pitches, planes equally spaced), else staged with 2-D copies; the match is enqueued on
 // `stream` and the maps are device images (asynchronous).
-void match(const std::vector<Image>& stack0, const std::vector<Image>& stack1, Image& disparity,
-           Config cfg, Image* corrmap, hipStream_t stream);
+void match(const std::vector<HipImage>& stack0, const std::vector<HipImage>& stack1, HipImage& disparity,
+           Config cfg, HipImage* corrmap, hipStream_t stream);
 
 }  // namespace BICOS::impl::hip

@@ -17,15 +17,14 @@
 // reference raised as std::invalid_argument, cpu.cpp:155).
 #pragma once
 
-#include <hip/hip_runtime_api.h>
 
 #include <vector>
 
-#include "common.hpp"
+#include "types.hpp"
 
 namespace BICOS {
 
-void match(const std::vector<Image>& stack0, const std::vector<Image>& stack1, Image& disparity,
-           Config cfg = Config{}, Image* corrmap = nullptr, hipStream_t stream = nullptr);
+void match(const std::vector<HipImage>& stack0, const std::vector<HipImage>& stack1, HipImage& disparity,
+           Config cfg = Config{}, HipImage* corrmap = nullptr, hipStream_t stream = nullptr);
 
 }  // namespace BICOS

@@ -13,26 +13,26 @@
 
 #include <vector>
 
-#include "common.hpp"
 #include "hip.hpp"
+#include "types.hpp"
 
 namespace BICOS {
 
 template <class MatT>
-Image image_view(const MatT& m) {
-    return Image(m.rows, m.cols, m.type(), (void*)m.data, (size_t)m.step[0], Memory::Host);
+HipImage image_view(const MatT& m) {
+    return HipImage(m.rows, m.cols, m.type(), (void*)m.data, (size_t)m.step[0], Memory::Host);
 }
 
 template <class MatT>
 void match_mats(const std::vector<MatT>& stack0, const std::vector<MatT>& stack1,
                 MatT& disparity, Config cfg = Config{}, MatT* corrmap = nullptr) {
-    std::vector<Image> s0, s1;
+    std::vector<HipImage> s0, s1;
     s0.reserve(stack0.size());
     s1.reserve(stack1.size());
     for (const MatT& m : stack0) s0.push_back(image_view(m));
     for (const MatT& m : stack1) s1.push_back(image_view(m));
     if (stack0.empty() || stack1.empty()) {
-        Image d;
+        HipImage d;
         impl::hip::match(s0, s1, d, cfg, nullptr, nullptr);  // throws the reference's error
         return;
     }
@@ -40,8 +40,8 @@ void match_mats(const std::vector<MatT>& stack0, const std::vector<MatT>& stack1
     const bool nxc = cfg.nxcorr_threshold.has_value();
     // allocate the outputs in the caller's type first, then let the engine fill them
     disparity.create(rows, cols, nxc ? (int)F32 : (int)S16);
-    Image d = image_view(disparity);
-    Image c;
+    HipImage d = image_view(disparity);
+    HipImage c;
     if (corrmap && nxc) {
         corrmap->create(rows, cols, cfg.precision == Precision::DOUBLE ? (int)F64 : (int)F32);
         c = image_view(*corrmap);

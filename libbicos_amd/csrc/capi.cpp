@@ -4,6 +4,7 @@
 #include <cstring>
 #include <vector>
 
+#include "../../include/bicos/common.hpp"
 #include "../../include/bicos/match.hpp"
 #include "../../include/bicos_c.h"
 #include "engine.hpp"

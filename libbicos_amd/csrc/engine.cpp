@@ -15,6 +15,7 @@
 #include <sstream>
 #include <vector>
 
+#include "../../include/bicos/common.hpp"
 #include "../../include/bicos/match.hpp"
 #include "../../include/bicos/hip.hpp"
 
@@ -1027,7 +1028,7 @@ const char* bicos_build_info(void) {
 
 namespace BICOS {
 
-size_t Image::elem_size(int type) {
+size_t HipImage::elem_size(int type) {
     switch (type) {
         case U8: return 1;
         case U16:
@@ -1038,12 +1039,12 @@ size_t Image::elem_size(int type) {
     throw Exception("unsupported image type " + std::to_string(type));
 }
 
-Image::Image(int rows, int cols, int type, void* data, size_t step, Memory mem)
+HipImage::HipImage(int rows, int cols, int type, void* data, size_t step, Memory mem)
     : _data(data), _rows(rows), _cols(cols), _type(type), _mem(mem) {
     _step = step ? step : (size_t)cols * elem_size(type);
 }
 
-void Image::create(int rows, int cols, int type, Memory mem) {
+void HipImage::create(int rows, int cols, int type, Memory mem) {
     // like cv::Mat::create: a no-op when the header already describes a dense buffer of this
     // size and type (owned or a view of the caller's memory), so results can be written
     // straight into caller-provided buffers
@@ -1069,7 +1070,7 @@ void Image::create(int rows, int cols, int type, Memory mem) {
     _mem = mem;
 }
 
-Image Image::download() const {
+HipImage HipImage::download() const {
     if (_mem == Memory::Host) return *this;
     Image h = allocate(_rows, _cols, _type, Memory::Host);
     if (!empty() &&
