@@ -13,6 +13,7 @@
 // the Consistency variant, --no-dupes then adds duplicate rejection). Divergence: the
 // reference declares --allow-negative-z but reads "allow-behind" (cli.cpp:233), so its flag
 // never takes effect; here it does.
+#include <bicos/common.hpp>
 #include <bicos/match.hpp>
 
 #include <chrono>

@@ -12,7 +12,8 @@
 //             <variant 0/1> <max_lr_diff> <no_dupes> <precision 0/1>
 // in.bin: int32 n, rows, cols, depth, then stack0 and stack1 as dense planes.
 // Writes <out_prefix>.<branch>.disp / .corr (raw, dense) and one line per branch on stdout.
-#include <bicos/match.hpp>
+// the reference's installed header name (no OpenCV here: BICOS::Image = BICOS::HipImage)
+#include <BICOS/match.hpp>
 #include <bicos/opencv.hpp>
 #include <hip/hip_runtime_api.h>
 

@@ -77,3 +77,87 @@ def test_cpp_match_branches_bit_exact(case, oracle, tmp_path):
         else:
             c = np.fromfile(cpath, dtype=rc.dtype).reshape(H, W)
             assert np.array_equal(c.view(np.uint8), rc.view(np.uint8)), b
+
+
+# ----------------------------------------- the reference's installed layout (include/BICOS)
+REF_EXE = os.path.join(ROOT, "build", "consumer", "ref_style")
+
+
+def install_and_build_consumer(prefix, bdir, quiet=True):
+    """cmake-install the in-tree libbicos_amd.so with the reference's header layout into
+    `prefix` (CMakeLists.txt, -DBICOS_PREBUILT_LIB), then configure and build the downstream
+    project tests/cpp/consumer (find_package(BICOS) + tests/cpp/ref_style.cpp) in `bdir`."""
+    lib = os.path.join(ROOT, "libbicos_amd", "libbicos_amd.so")
+    kw = dict(check=True, capture_output=quiet)
+    subprocess.run(["cmake", "-S", ROOT, "-B", os.path.join(bdir, "pkg"),
+                    "-DBICOS_PREBUILT_LIB=" + lib, "-DCMAKE_INSTALL_PREFIX=" + prefix], **kw)
+    subprocess.run(["cmake", "--install", os.path.join(bdir, "pkg")], **kw)
+    subprocess.run(["cmake", "-S", os.path.join(ROOT, "tests", "cpp", "consumer"), "-B", bdir,
+                    "-DCMAKE_PREFIX_PATH=" + prefix], **kw)
+    subprocess.run(["cmake", "--build", bdir], **kw)
+    return os.path.join(bdir, "ref_style")
+
+
+def test_installed_tree_has_the_reference_layout_and_builds_a_reference_caller(tmp_path):
+    """include/BICOS/{common,match,config}.hpp + libBICOS.so / pybicos_c.so next to
+    libbicos_amd.so (reference CMakeLists.txt:82-104), and a translation unit written against
+    the reference's names only (#include <BICOS/match.hpp>, BICOS::Image = cv::Mat,
+    BICOS::match / Config / Variant / is_invalid) builds unchanged against the installed tree
+    through find_package(BICOS). CPU only: nothing is run."""
+    prefix = str(tmp_path / "prefix")
+    exe = install_and_build_consumer(prefix, str(tmp_path / "consumer"))
+    for h in ("common.hpp", "match.hpp", "config.hpp"):
+        assert os.path.exists(os.path.join(prefix, "include", "BICOS", h)), h
+    lib = os.path.join(prefix, "lib")
+    assert os.path.realpath(os.path.join(lib, "libBICOS.so")) == \
+        os.path.realpath(os.path.join(lib, "libbicos_amd.so"))
+    assert os.path.realpath(os.path.join(lib, "pybicos_c.so")) == \
+        os.path.realpath(os.path.join(lib, "libbicos_amd.so"))
+    assert os.access(exe, os.X_OK)
+    cfg = open(os.path.join(prefix, "include", "BICOS", "config.hpp")).read()
+    assert "#define BICOS_HIP" in cfg and "BICOS_VERSION" in cfg
+
+
+REF_CASES = [
+    dict(n=33, H=20, W=400, cfg=dict(nxcorr_threshold=0.96, min_variance=2.0, subpixel_step=0.1)),
+    dict(n=8, H=30, W=256, cfg=dict(nxcorr_threshold=None)),
+    dict(n=40, H=12, W=300, cfg=dict(nxcorr_threshold=0.9, variant=1, max_lr_diff=1)),
+    dict(n=12, H=16, W=200, cfg=dict(nxcorr_threshold=0.5, mode=1, variant=1, max_lr_diff=2,
+                                     no_dupes=True)),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", REF_CASES, ids=lambda c: "n%d_%dx%d" % (c["n"], c["H"], c["W"]))
+def test_reference_style_caller_bit_exact(case, oracle, tmp_path):
+    """The reference-style TU (built by build() against the installed tree) matches the oracle
+    bit for bit through BICOS::match on cv::Mat stacks."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no ROCm GPU")
+    assert os.access(REF_EXE, os.X_OK), "build() builds build/consumer/ref_style"
+    n, H, W, cfg = case["n"], case["H"], case["W"], case["cfg"]
+    L, R = stereo_stack(n, H, W, np.uint8)
+    inp = tmp_path / "in.bin"
+    with open(inp, "wb") as f:
+        f.write(np.array([n, H, W, 1], np.int32).tobytes())
+        f.write(np.ascontiguousarray(L).tobytes())
+        f.write(np.ascontiguousarray(R).tobytes())
+    g = cfg.get
+    nxc = g("nxcorr_threshold")
+    args = [REF_EXE, str(inp), str(tmp_path / "out"), str(-1 if nxc is None else nxc),
+            str(g("subpixel_step") or -1), str(-1 if g("min_variance") is None else g("min_variance")),
+            str(0 if g("mode", 0) else 1), str(g("variant", 0)), str(g("max_lr_diff", 1)),
+            str(int(g("no_dupes", False)))]
+    r = subprocess.run(args, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    rd, rc = oracle.match(L, R, oracle.OracleConfig(**cfg))
+    d = np.fromfile(tmp_path / "out.ref.disp", dtype=rd.dtype).reshape(H, W)
+    assert np.array_equal(d.view(np.uint8), rd.view(np.uint8))
+    cpath = tmp_path / "out.ref.corr"
+    if rc is None:
+        assert not cpath.exists()
+    else:
+        c = np.fromfile(cpath, dtype=rc.dtype).reshape(H, W)
+        assert np.array_equal(c.view(np.uint8), rc.view(np.uint8))
+    assert ("type=%d" % (3 if rc is None else 5)) in r.stdout
