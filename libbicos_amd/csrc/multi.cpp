@@ -63,6 +63,34 @@ struct FirstError {
     int raise() { return code == BICOS_OK ? BICOS_OK : fail(code, msg); }
 };
 
+// Stage slots of one band's maps, appended at `off` (which advances past them): the
+// disparity map, then (csz != 0) the corrmap, each 256-byte aligned with 256 bytes of slack.
+// The reservation and the enqueue loop of bicos_match_bands_device both walk the bands with
+// this one function, so the bytes reserved always cover the offsets written.
+void band_stage_offsets(size_t& off, int rows, int cols, size_t dsz, size_t csz, size_t* od,
+                        size_t* oc) {
+    auto slot = [&](size_t bytes) {
+        const size_t at = off;
+        off = (off + bytes + 256 + 255) / 256 * 256;
+        return at;
+    };
+    *od = slot((size_t)rows * cols * dsz);
+    *oc = csz ? slot((size_t)rows * cols * csz) : 0;
+}
+
+// Let `peer` read and write memory of `owner`'s default stream-ordered pool (hipMallocAsync,
+// which peer access does not cover).
+int share_pool(int owner, int peer) {
+    hipMemPool_t pool = nullptr;
+    int rc = check_hip(hipDeviceGetDefaultMemPool(&pool, owner), "hipDeviceGetDefaultMemPool");
+    if (rc) return rc;
+    hipMemAccessDesc d{};
+    d.location.type = hipMemLocationTypeDevice;
+    d.location.id = peer;
+    d.flags = hipMemAccessFlagsProtReadWrite;
+    return check_hip(hipMemPoolSetAccess(pool, &d, 1), "hipMemPoolSetAccess");
+}
+
 float nxc_threshold(const BicosConfig& cfg) {
     // reference src/pybicos_c.cpp:59-61: a negative threshold keeps the default 0.5
     return cfg.nxcorr_threshold >= 0 ? cfg.nxcorr_threshold : 0.5f;
@@ -174,9 +202,14 @@ extern "C" int bicos_match_bands_device(const int* devices, int ndev, const void
         // band 0 (on the root) writes straight into the maps; every other band's maps go to
         // its engine's stage and are peer-copied (a band placed on the root again -- devices
         // may repeat -- takes the same path with a device-local copy)
+        // stage layout per device: the same offsets the enqueue loop below takes
+        // (band_stage_offsets), so the reservation covers the last byte written
         std::map<int, size_t> stage_need;
-        for (int b = 1; b < ndev; ++b)
-                stage_need[devices[b]] += 2 * (size_t)band_rows[b] * cols * (dsz + (corrmap ? csz : 0)) + 512;
+        for (int b = 1; b < ndev; ++b) {
+            size_t sd = 0, sc = 0;
+            band_stage_offsets(stage_need[devices[b]], band_rows[b], cols, dsz, corrmap ? csz : 0,
+                               &sd, &sc);
+        }
         for (auto& kv : stage_need) {
             bicos_engine* e = engines[kv.first];
             rc = reserve(e->stage, e->stage_bytes, kv.second, e->device, e->own_stream, e->ws_ready);
@@ -190,6 +223,11 @@ extern "C" int bicos_match_bands_device(const int* devices, int ndev, const void
                     if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled)
                         rc = check_hip(pe, "hipDeviceEnablePeerAccess");
                     (void)hipGetLastError();  // clear a sticky "already enabled"
+                    // peer access does not cover stream-ordered pool memory: the stage comes
+                    // from this device's default pool (hipMallocAsync) and the root's maps may
+                    // too, so grant each device access to the other's pool explicitly
+                    if (!rc) rc = share_pool(e->device, root);
+                    if (!rc) rc = share_pool(root, e->device);
                 }
             }
             if (rc) {
@@ -218,16 +256,10 @@ extern "C" int bicos_match_bands_device(const int* devices, int ndev, const void
                                   depth, *cfg, has_nxcorr != 0, thr, dst_d, dst_c, e->own_stream);
                 continue;
             }
-            size_t& off = used[devices[b]];
-            char* sd = (char*)e->stage + off;
-            off += (size_t)br * cols * dsz + 256;
-            off = (off + 255) / 256 * 256;
-            char* sc = nullptr;
-            if (corrmap) {
-                sc = (char*)e->stage + off;
-                off += (size_t)br * cols * csz + 256;
-                off = (off + 255) / 256 * 256;
-            }
+            size_t od = 0, oc = 0;
+            band_stage_offsets(used[devices[b]], br, cols, dsz, corrmap ? csz : 0, &od, &oc);
+            char* sd = (char*)e->stage + od;
+            char* sc = corrmap ? (char*)e->stage + oc : nullptr;
             rc = match_device(e, stack0[b], stack1[b], n, br, cols, row_pitch[b], plane_pitch[b],
                               depth, *cfg, has_nxcorr != 0, thr, sd, sc, e->own_stream);
             if (!rc)

@@ -139,3 +139,20 @@ def test_bands_device_repeated_calls_reuse_the_stage(gpu):
         dm, cm = match_bands([s0[:, r0:r1] for r0, r1 in b], [s1[:, r0:r1] for r0, r1 in b], cfg)
         same(host(dm), host(d1))
         same(host(cm), host(c1))
+
+
+@pytest.mark.parametrize("W,kw", [(1, {}), (3, {"precision": 1}), (5, {"nxcorr_threshold": None})])
+def test_bands_device_one_row_bands_of_narrow_frames(gpu, W, kw):
+    """Nine one-row bands of a 1-5 column frame, all but the first through the stage: the
+    per-band slack (256-byte slots) dominates the stage size here, the case where a stage
+    reserved by a different formula than the enqueue loop's offsets was overrun."""
+    from libbicos_amd.device import MatchConfig, match_bands
+    L, R = stereo_stack(8, 9, W, dmin=0, drange=2)
+    s0, s1 = dev(L), dev(R)
+    cfg = MatchConfig(**kw)
+    d1, c1 = gpu.match(s0, s1, cfg)
+    b = _bands(9, 9)
+    dm, cm = match_bands([s0[:, r0:r1] for r0, r1 in b], [s1[:, r0:r1] for r0, r1 in b], cfg)
+    same(host(dm), host(d1))
+    if c1 is not None:
+        same(host(cm), host(c1))
