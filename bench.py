@@ -90,29 +90,19 @@ CONFIGS = {
 
 
 def search_pairs(rows: int, W: int, cfg: dict) -> float:
-    """Hamming pairs per match: every (col0, col1) of every row, i.e. the cost matrix. With
-    Consistency the reference searches it twice (forward, then reverse from each best
-    col1); the fused kernel evaluates each entry once and takes row and column minima, so
-    the algorithmic count stays rows * W^2."""
+    """Hamming pairs of one pass over the cost matrix: every (col0, col1) of every row.
+    Consistency searches it twice (forward, then the full reverse; callers double it)."""
     return float(rows) * W * W
 
 
 def search_pair_peak(words: int, cfg: dict) -> float:
-    """Issue-rate bound in pairs/s of the search kernel's per-pair instruction mix at the
-    measured VALU rates. Forward (search16_kernel): `words` v_xor (full rate) + `words`
-    v_bcnt (half rate) + half a v_perm and half a v_pk_min_u16 (2 col0 share one packed
-    key register) + with duplicate detection another half v_xor (full) and half
-    v_pk_min_u16 (half). Consistency (search_lr_kernel, 4 col0 per lane) adds the column
-    minima: 1 v_lshl_or + 1/2 v_min3 per pair and per col1 a 6-step DPP v_min reduction
-    (6/4 half-rate per pair) + ~3 full-rate ops (3/4 per pair); all doubled with NoDuplicates."""
-    consistency = cfg.get("variant", 0) == 1
-    dupes = not consistency or cfg.get("no_dupes", False)
+    """Issue-rate bound in pairs/s of the VALU search's per-pair instruction mix at the
+    measured VALU rates (search16_kernel): `words` v_xor (full rate) + `words` v_bcnt (half
+    rate) + half a v_perm and half a v_pk_min_u16 (2 col0 share one packed key register) +
+    with duplicate detection another half v_xor (full) and half v_pk_min_u16 (half)."""
+    dupes = cfg.get("variant", 0) == 0 or cfg.get("no_dupes", False)
     full = words + (0.5 if dupes else 0.0)
     half = words + 1.0 + (0.5 if dupes else 0.0)
-    if consistency:
-        k = 2.0 if dupes else 1.0
-        full += 0.75 * k
-        half += (1.0 + 0.5 + 1.5) * k
     per_pair_s = full / (VALU_FULL_TOPS * 1e12) + half / (VALU_HALF_TOPS * 1e12)
     return 1.0 / per_pair_s
 
@@ -708,12 +698,6 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     flags = (2 | (1 if mcfg.no_dupes else 0)) if mcfg.variant == 1 else 1
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(6)]
     mc = C["cfg"]
-    # the pipeline fuses the NXC agree into the search epilogue (engine.cpp match_device)
-    # only with the VALU search (BICOS_SEARCH=valu) unless BICOS_FUSE_AGREE=0
-    fuse_env = os.environ.get("BICOS_FUSE_AGREE", "")
-    fused_agree = (mcfg.variant == 0 and mcfg.nxcorr_threshold is not None and
-                   not mc.get("subpixel_step") and not mcfg.precision and
-                   (fuse_env == "1" if mx_search() else fuse_env != "0"))
     mv = mc.get("min_variance")
     mv = None if mv is None or mv < 0 else mv * n
     from libbicos_amd import device
@@ -721,11 +705,8 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     sbits = transform_bits(n, mcfg.mode)
 
     def search_launch():
-        if fused_agree:
-            eng.search_agree(d0, d1, s0, s1, words, mcfg.nxcorr_threshold, minvar_scaled=mv)
-        else:
-            # with the used-bits hint the pipeline passes (engine.cpp match_device)
-            eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw, bits=ubits)
+        # with the used-bits hint the pipeline passes (engine.cpp match_device)
+        eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw, bits=ubits)
 
     reps = args.kernel_reps
     search_launch()  # warm
@@ -736,12 +717,8 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     for _ in range(reps):
         eng.transform(s0, mcfg.mode, words, out=d0)
     ev[2].record(st)
-    if fused_agree:  # the standalone agree below needs the int16 search result
-        eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw)
     thr = mc.get("nxcorr_threshold")
     stage = "subpixel" if mc.get("subpixel_step") else "nxcorr"
-    if fused_agree:
-        stage = "nxcorr (standalone agree kernel; the pipeline runs it fused in the search)"
     ev[3].record(st)
     for _ in range(reps):
         eng.agree(raw, s0, s1, 0.96 if thr is None else thr, minvar_scaled=mv,
@@ -761,7 +738,7 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     search_bytes = rows * W * (2 * 4 * words + 2)
     mx = mx_search()
     cons = mc.get("variant", 0) == 1
-    kname = "search_mx_kernel" if mx else ("search_lr_kernel" if cons else "search16_kernel")
+    kname = "search_mx_kernel" if mx else "search16_kernel"
     cfgname = args.config
     traffic = load_traffic(kname, cfgname, rows)
     if mx:
@@ -774,7 +751,7 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
             "kernel": ("search_mx_kernel<%d words> x2 (forward + reverse FP4 MFMA Hamming argmin) "
                        "+ consistency_kernel" % words if cons else
                        "search_mx_kernel<%d words> (FP4 MFMA Hamming products, argmin keys in the "
-                       "accumulator)%s" % (words, " + fused NXC agree epilogue" if fused_agree else "")),
+                       "accumulator)" % words),
             "bound": "mfma",
             "achieved": round(achieved_tf, 1),
             "peak": MFMA_FP4_DENSE_TFLOPS,
@@ -811,13 +788,13 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
             },
         }
     else:
+        pairs *= 2 if cons else 1  # two passes with Consistency
         achieved = pairs / t_search / 1e9
         peak = search_pair_peak(words, mc) / 1e9
         roof = {
-            "kernel": ("search_lr_kernel<%d words> (fused forward + reverse Hamming argmin)" % words
+            "kernel": ("search16_kernel<%d words> x2 (forward + reverse Hamming argmin)" % words
                        if cons else
-                       "search16_kernel<%d words> (Hamming argmin, packed 16-bit keys)%s" %
-                       (words, " + fused NXC agree epilogue" if fused_agree else "")),
+                       "search16_kernel<%d words> (Hamming argmin, packed 16-bit keys)" % words),
             "bound": "valu",
             "achieved": round(achieved, 1),
             "peak": round(peak, 1),
@@ -832,7 +809,7 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
                           "(full %.1f / half %.1f T lane-op/s); see DESIGN.md s5" %
                           (VALU_FULL_TOPS, VALU_HALF_TOPS),
             "lane_ops_view": {
-                "achieved_Tops": round(search_ops(rows, W, words, mc) / t_search / 1e12, 2),
+                "achieved_Tops": round(search_ops(rows, W, words, mc) * (2 if cons else 1) / t_search / 1e12, 2),
                 "nominal_peak_Tops": round(VALU_NOMINAL_TOPS, 1),
                 "ops_model": "one pass over the cost matrix, 32-bit keys: 2w+3 (2w+2) lane-ops per pair",
             },

@@ -227,15 +227,6 @@ int bicos_subpixel_device(const int16_t* raw, const void* stack0, const void* st
                           float threshold, float step, int has_minvar, float minvar_scaled,
                           float* out, float* corrmap, void* stream);
 
-/* NoDuplicates search with the NXC agree fused into its epilogue (what bicos_match_device
- * runs without Consistency / subpixel / DOUBLE): out = float disparity (-32768 invalid),
- * corrmap float (NaN where no correlation), or NULL; minvar_scaled = min_variance * n. */
-int bicos_search_agree_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* desc1,
-                              const void* stack0, const void* stack1, int n, int rows, int cols,
-                              size_t row_pitch, size_t plane_pitch, int depth, int words,
-                              float threshold, int has_minvar, float minvar_scaled, float* out,
-                              float* corrmap, void* stream);
-
 /* Build identification (arch, flags) for reports. */
 const char* bicos_build_info(void);
 

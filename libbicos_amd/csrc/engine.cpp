@@ -141,47 +141,6 @@ bicos_hip::MxGeometry mx_geometry(const bicos_engine* e, int rows, int cols, int
                                          tuned ? e->tune_variant - 64 : 0, bits);
 }
 
-// The NoDuplicates search with the NXC agree fused into its epilogue (sa.out_f32 set): the
-// matrix-core kernel unless BICOS_SEARCH=valu / a VALU tuning; a non-default VALU variant
-// runs variant 16.
-int launch_search_agree(const bicos_engine* e, const bicos_hip::SearchArgs& sa, int words,
-                        hipStream_t st) {
-    if (use_mx(e)) {
-        const bicos_hip::MxGeometry gm = mx_geometry(e, sa.rows, sa.cols, words);
-        return check_hip(bicos_hip::launch_search_mx(sa, gm, words, true, st),
-                         "search + agree launch");
-    }
-    bicos_hip::SearchGeometry g = geometry(e, sa.rows, sa.cols, words);
-    if (g.variant != 16)
-        g = bicos_hip::search_geometry(sa.rows, sa.cols, words, e ? e->max_lds : 64 * 1024);
-    return check_hip(bicos_hip::launch_search(sa, g, words, true, st), "search + agree launch");
-}
-
-bool fused_consistency() {
-    // one fused forward+reverse search (search_lr_kernel) unless BICOS_CONSISTENCY=twopass
-    // asks for a forward and a full reverse search (A/B; identical results)
-    static const bool twopass = [] {
-        const char* v = std::getenv("BICOS_CONSISTENCY");
-        return v && !std::strcmp(v, "twopass");
-    }();
-    return !twopass;
-}
-
-bicos_hip::SearchGeometry geometry_lr(const bicos_engine* e, int rows, int cols, int words,
-                                      bool nodupes) {
-    // row stage + one (two with NoDuplicates) 32-bit column key per col1; up to 80 KiB so a
-    // 256-bit 2048-column row stays one stage with 2 workgroups per CU (160 KiB LDS)
-    const int limit = e ? e->lds_limit : 64 * 1024;
-    const int budget = limit < 80 * 1024 ? limit : 80 * 1024;
-    const int extra = 4 * (nodupes ? 2 : 1);
-    if (!e || e->tune_variant >= 64)
-        return bicos_hip::search_geometry(rows, cols, words, budget, 16, 4, 0, 0, 256, extra);
-    // 4 col0 per lane by default: the per-col1 wave reduction amortises over more pairs
-    const int R = (e->tune_R == 2 || e->tune_R == 4) ? e->tune_R : 4;
-    return bicos_hip::search_geometry(rows, cols, words, budget, 16, R, e->tune_waves,
-                                      e->tune_split, e->cus, extra);
-}
-
 // Number of x the reference's subpixel loop visits: for (float x = -1.f; x <= 1.f; x += step)
 // (agree.hpp:122 / agree.cuh:213), accumulated in float exactly as there. 0 when the loop
 // would exceed MAX_SUBPIXEL_STEPS (or never end: x + step == x), which the reference would
@@ -249,17 +208,12 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     const bool dbl = cfg.precision != 0;
 
     const bool mx = use_mx(e);
-    const bool fused = consistency && !mx && fused_consistency();
-    const bicos_hip::SearchGeometry glr =
-        fused ? geometry_lr(e, rows, cols, words, nodupes) : bicos_hip::SearchGeometry{};
 
-    // workspace: desc0 | desc1 | raw int16 | fwd | rev (two-pass) or rev keys (fused)
+    // workspace: desc0 | desc1 | raw int16 | fwd | rev (Consistency)
     const size_t dpitch = bicos_desc_pitch(cols, words);
     const size_t desc_bytes = align_up((size_t)rows * dpitch * 4);
     const size_t map16 = align_up((size_t)rows * cols * 2);
-    const size_t keys = fused ? align_up((size_t)rows * glr.tiles_per_row * cols * 4) : 0;
-    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) +
-                  (consistency ? (fused ? map16 + keys * (nodupes ? 2 : 1) : 2 * map16) : 0);
+    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) + (consistency ? 2 * map16 : 0);
     int rc = reserve(e->ws, e->ws_bytes, need, e->device, st, e->ws_ready);
     if (rc) return rc;
     // order against earlier users of ws / stage on other streams; mark our use on exit
@@ -278,114 +232,32 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     int16_t* raw = has_nxcorr ? (int16_t*)p : (int16_t*)disp;
     if (has_nxcorr) p += map16;
     int16_t* fwd = consistency ? (int16_t*)p : nullptr;
-    int16_t* rev = consistency && !fused ? (int16_t*)(p + map16) : nullptr;
-    uint32_t* rev_first = fused ? (uint32_t*)(p + map16) : nullptr;
-    uint32_t* rev_last = fused && nodupes ? (uint32_t*)(p + map16 + keys) : nullptr;
-
-    // Fused transform -> search (BICOS_FUSE_TRANSFORM=1): the
-    // matrix-core NoDuplicates search computes the LIMITED descriptors from the stacks
-    // itself (no descriptor round trip through HBM, no transform launch). Measured slower
-    // than the two kernels, so opt-in: every search workgroup re-derives the
-    // whole right row it scans.
-    const bool fuse_tf_env = [] {  // read per call (tests toggle it)
-        const char* v = std::getenv("BICOS_FUSE_TRANSFORM");
-        return v && !std::strcmp(v, "1");
-    }();
-    const bool fuse_tf = fuse_tf_env && mx && !consistency && mode == 0 && words <= 4 &&
-                         cols <= 8160;
+    int16_t* rev = consistency ? (int16_t*)(p + map16) : nullptr;
 
     // 1. descriptor_transform, both stacks in one launch (cpu.cpp:50-59)
-    if (!fuse_tf) {
-        bicos_hip::TransformArgs ta{s0, s1, d0, d1, n, rows, cols, row_pitch, plane_pitch, dpitch, 0, span};
-        rc = check_hip(bicos_hip::launch_transform(ta, depth, mode, words, st), "transform launch");
-        if (rc) return rc;
-    }
+    bicos_hip::TransformArgs ta{s0, s1, d0, d1, n, rows, cols, row_pitch, plane_pitch, dpitch, 0, span};
+    rc = check_hip(bicos_hip::launch_transform(ta, depth, mode, words, st), "transform launch");
+    if (rc) return rc;
 
-    // 2. bicos search (cpu.cpp:68-75)
-    const bicos_hip::SearchGeometry g = mx ? bicos_hip::SearchGeometry{} : geometry(e, rows, cols, words);
-    // NXC agree fused into the search epilogue (no Consistency, no subpixel, single
-    // precision): BICOS_FUSE_AGREE unset = with the VALU search (variant 16) only -- the
-    // matrix-core search runs faster with the separate agree kernel (measured: cfg2 fused
-    // 0.580 ms vs 0.437 + 0.061 separate); 1 = with either search; 0 = never
-    static const int fuse_env = [] {
-        const char* v = std::getenv("BICOS_FUSE_AGREE");
-        if (v && !std::strcmp(v, "0")) return 0;
-        if (v && !std::strcmp(v, "1")) return 2;
-        return 1;
-    }();
-    const bool has_step_ = has_nxcorr && cfg.subpixel_step >= 0;
-    const bool fuse_agree = fuse_env && !consistency && has_nxcorr && !has_step_ && !dbl && !disp_i16 &&
-                            (mx ? fuse_env == 2 : g.variant == 16);
-    if (fuse_agree && !fuse_tf) {
-        bicos_hip::SearchArgs sa{d0, d1, nullptr, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
-        sa.out_f32 = (float*)disp;
-        sa.corr = (float*)corr;
-        sa.stack0 = s0;
-        sa.stack1 = s1;
-        sa.n = n;
-        sa.depth = depth;
-        sa.row_pitch = row_pitch;
-        sa.plane_pitch = plane_pitch;
-        sa.threshold = threshold;
-        sa.has_minvar = cfg.min_variance >= 0;
-        sa.minvar = sa.has_minvar ? cfg.min_variance * (float)n : 0.f;  // cpu.cpp:127
-        return launch_search_agree(e, sa, words, st);
-    }
-    if (mx) {
-        const bicos_hip::MxGeometry gm = mx_geometry(e, rows, cols, words, used_bits(n, mode));
-        if (!consistency) {
-            bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
-            if (fuse_tf) {
-                sa.fused_tf = 1;
-                sa.stack0 = s0;
-                sa.stack1 = s1;
-                sa.n = n;
-                sa.depth = depth;
-                sa.row_pitch = row_pitch;
-                sa.plane_pitch = plane_pitch;
-                sa.stack_bytes = span;
-                sa.tf_magic = (uint32_t)((0x100000000ull + (uint64_t)n - 1) / (uint64_t)n);
-            }
-            rc = check_hip(bicos_hip::launch_search_mx(sa, gm, words, true, st),
-                           fuse_tf ? "fused transform + search launch" : "search launch");
-            if (rc) return rc;
-        } else {
-            // forward and full reverse search (reverse = the same search with the stacks
-            // swapped, bicos.hpp:96), then the left-right check
-            bicos_hip::SearchArgs fa{d0, d1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
-            rc = check_hip(bicos_hip::launch_search_mx(fa, gm, words, nodupes, st), "search launch");
-            if (rc) return rc;
-            bicos_hip::SearchArgs ra{d1, d0, rev, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
-            rc = check_hip(bicos_hip::launch_search_mx(ra, gm, words, nodupes, st),
-                           "reverse search launch");
-            if (rc) return rc;
-            bicos_hip::ConsistencyArgs ca{fwd, rev, raw, rows, cols, (size_t)cols, cfg.max_lr_diff};
-            rc = check_hip(bicos_hip::launch_consistency(ca, st), "consistency launch");
-            if (rc) return rc;
-        }
-    } else if (!consistency) {
-        bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
-        rc = check_hip(bicos_hip::launch_search(sa, g, words, true, st), "search launch");
-        if (rc) return rc;
-    } else if (fused) {
-        bicos_hip::SearchArgs fa{d0, d1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
-        fa.rev_first = rev_first;
-        fa.rev_last = rev_last;
-        rc = check_hip(bicos_hip::launch_search_lr(fa, glr, words, nodupes, st),
-                       "fused consistency search launch");
-        if (rc) return rc;
-        bicos_hip::ConsistencyArgs ca{fwd, nullptr, raw, rows, cols, (size_t)cols, cfg.max_lr_diff};
-        ca.rev_first = rev_first;
-        ca.rev_last = rev_last;
-        ca.rev_tiles = glr.tiles_per_row;
-        rc = check_hip(bicos_hip::launch_consistency_keys(ca, st), "consistency launch");
+    // 2. bicos search (cpu.cpp:68-75): NoDuplicates in one search; Consistency as the
+    // forward and the full reverse search (the same search with the stacks swapped,
+    // bicos.hpp:96), then the left-right check
+    auto search = [&](const uint32_t* a0, const uint32_t* a1, int16_t* out, int out_mode,
+                      bool nd, const char* what) {
+        bicos_hip::SearchArgs sa{a0, a1, out, rows, cols, dpitch, (size_t)cols, out_mode, 0, 0, 0};
+        if (mx)
+            return check_hip(bicos_hip::launch_search_mx(
+                                 sa, mx_geometry(e, rows, cols, words, used_bits(n, mode)), words, nd, st),
+                             what);
+        return check_hip(bicos_hip::launch_search(sa, geometry(e, rows, cols, words), words, nd, st),
+                         what);
+    };
+    if (!consistency) {
+        rc = search(d0, d1, raw, 0, true, "search launch");
         if (rc) return rc;
     } else {
-        bicos_hip::SearchArgs fa{d0, d1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
-        rc = check_hip(bicos_hip::launch_search(fa, g, words, nodupes, st), "search launch");
-        if (rc) return rc;
-        bicos_hip::SearchArgs ra{d1, d0, rev, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
-        rc = check_hip(bicos_hip::launch_search(ra, g, words, nodupes, st), "reverse search launch");
+        rc = search(d0, d1, fwd, 1, nodupes, "search launch");
+        if (!rc) rc = search(d1, d0, rev, 1, nodupes, "reverse search launch");
         if (rc) return rc;
         bicos_hip::ConsistencyArgs ca{fwd, rev, raw, rows, cols, (size_t)cols, cfg.max_lr_diff};
         rc = check_hip(bicos_hip::launch_consistency(ca, st), "consistency launch");
@@ -879,32 +751,6 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     if (!e) return fail(BICOS_E_ARG, "consistency search needs an engine workspace");
     std::lock_guard<std::mutex> lk(e->lock);  // the workspace may be shared (default engine)
     const size_t map16 = align_up((size_t)rows * cols * 2);
-    if (!mx && fused_consistency()) {
-        const bicos_hip::SearchGeometry glr = geometry_lr(e, rows, cols, words, nodupes);
-        const size_t keys = align_up((size_t)rows * glr.tiles_per_row * cols * 4);
-        int rc = reserve(e->ws, e->ws_bytes, map16 + keys * (nodupes ? 2 : 1), e->device, st,
-                         e->ws_ready);
-        if (rc) return rc;
-        rc = check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent");
-        if (rc) return rc;
-        int16_t* fwd = (int16_t*)e->ws;
-        uint32_t* rev_first = (uint32_t*)((char*)e->ws + map16);
-        uint32_t* rev_last = nodupes ? (uint32_t*)((char*)e->ws + map16 + keys) : nullptr;
-        bicos_hip::SearchArgs fa{desc0, desc1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
-        fa.rev_first = rev_first;
-        fa.rev_last = rev_last;
-        rc = check_hip(bicos_hip::launch_search_lr(fa, glr, words, nodupes, st),
-                       "fused consistency search launch");
-        if (!rc) {
-            bicos_hip::ConsistencyArgs ca{fwd, nullptr, out, rows, cols, (size_t)cols, max_lr_diff};
-            ca.rev_first = rev_first;
-            ca.rev_last = rev_last;
-            ca.rev_tiles = glr.tiles_per_row;
-            rc = check_hip(bicos_hip::launch_consistency_keys(ca, st), "consistency launch");
-        }
-        (void)hipEventRecord(e->ws_ready, st);
-        return rc;
-    }
     int rc = reserve(e->ws, e->ws_bytes, 2 * map16, e->device, st, e->ws_ready);
     if (rc) return rc;
     rc = check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent");
@@ -932,36 +778,6 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     if (rc) return rc;
     bicos_hip::ConsistencyArgs ca{fwd, rev, out, rows, cols, (size_t)cols, max_lr_diff};
     return check_hip(bicos_hip::launch_consistency(ca, st), "consistency launch");
-}
-
-int bicos_search_agree_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* desc1,
-                              const void* stack0, const void* stack1, int n, int rows, int cols,
-                              size_t row_pitch, size_t plane_pitch, int depth, int words,
-                              float threshold, int has_minvar, float minvar_scaled, float* out,
-                              float* corrmap, void* stream) {
-    if (words != 1 && words != 2 && words != 4 && words != 8)
-        return fail(BICOS_E_ARG, "words must be 1, 2, 4 or 8");
-    if (n < 2) return fail(BICOS_E_ARG, "need at least two images");
-    if (depth != 1 && depth != 2) return fail(BICOS_E_ARG, "bad input depth");
-    if (cols > 32767) return fail(BICOS_E_ARG, "image width exceeds 32767");
-    if (rows <= 0 || cols <= 0) return BICOS_OK;
-    if (!desc0 || !desc1 || !stack0 || !stack1 || !out) return fail(BICOS_E_ARG, "null buffer");
-    if (row_pitch < (size_t)cols || plane_pitch < (size_t)rows * row_pitch)
-        return fail(BICOS_E_ARG, "row/plane pitch smaller than the image");
-    bicos_hip::SearchArgs sa{desc0, desc1, nullptr, rows, cols, bicos_desc_pitch(cols, words),
-                             (size_t)cols, 0, 0, 0};
-    sa.out_f32 = out;
-    sa.corr = corrmap;
-    sa.stack0 = stack0;
-    sa.stack1 = stack1;
-    sa.n = n;
-    sa.depth = depth;
-    sa.row_pitch = row_pitch;
-    sa.plane_pitch = plane_pitch;
-    sa.threshold = threshold;
-    sa.has_minvar = has_minvar;
-    sa.minvar = minvar_scaled;
-    return launch_search_agree(e, sa, words, (hipStream_t)stream);
 }
 
 static int agree_common(bool sub, const int16_t* raw, const void* stack0, const void* stack1,

@@ -3,7 +3,6 @@
 //   transform_kernel    descriptor_transform  (reference include/impl/cpu/descriptor_transform.hpp:31-138)
 //   search16_kernel     bicos Hamming search on the VALU (reference include/impl/cpu/bicos.hpp:29-113;
 //                       the default search runs on the matrix cores: search_mx.hip)
-//   search_lr_kernel    the same, Consistency's forward + reverse minima in one pass
 //   consistency_kernel  left-right check      (reference include/impl/cpu/bicos.hpp:99-106)
 //   agree_kernel        NXC filter            (reference include/impl/cpu/agree.hpp:28-93)
 //   (subpixel_kernel, the NXC + quadratic refine of agree.hpp:95-191: subpixel.hpp)
@@ -200,6 +199,31 @@ __global__ __launch_bounds__(256) void transform_limited_kernel(TransformArgs a)
     }
 }
 
+// Four u8 pixels per lane (transform.hpp limited_descriptor4): one dword load per plane
+// instead of four byte loads; used for u8 LIMITED stacks whose columns, pitches and bases
+// are multiples of 4 (launch_transform), the one-pixel kernel above otherwise.
+template <int WORDS, int MAXN, bool EXACT>
+__global__ __launch_bounds__(256) void transform4_kernel(TransformArgs a) {
+    const int col4 = (blockIdx.x * 256 + threadIdx.x) * 4;
+    const int row = blockIdx.y;
+    const int which = blockIdx.z;
+    if (col4 >= a.cols) return;
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<void*>(which ? a.stack1 : a.stack0), (short)0, (int)a.stack_bytes, 0x00020000);
+    uint32_t* __restrict__ out = (which ? a.desc1 : a.desc0) + (size_t)row * a.desc_pitch + (size_t)col4 * WORDS;
+    uint32_t w[4][WORDS];
+    limited_descriptor4<WORDS, MAXN, EXACT>(r, (uint32_t)col4, (uint32_t)row * (uint32_t)a.row_pitch,
+                                            (uint32_t)a.plane_pitch, a.n, a.magic, w);
+    // the 4 pixels' 4 x WORDS words are contiguous and 16-byte aligned (desc_pitch % 4 == 0)
+#pragma unroll
+    for (int q = 0; q < WORDS; ++q) {
+        const int f = 4 * q;  // flat word index f .. f+3 of [pixel][word]
+        *(uint4*)(out + f) = make_uint4(w[f / WORDS][f % WORDS], w[(f + 1) / WORDS][(f + 1) % WORDS],
+                                        w[(f + 2) / WORDS][(f + 2) % WORDS],
+                                        w[(f + 3) / WORDS][(f + 3) % WORDS]);
+    }
+}
+
 // --------------------------------------------------------------------- search
 
 // Hamming cost of one (col0, col1) pair.
@@ -281,9 +305,9 @@ __device__ __forceinline__ void search16_step(const uint32_t* s, uint32_t seed,
     }
 }
 
-// FUSE: 0 = plain search (int16 `out`), 1 / 2 = fused NXC agree epilogue on u8 / u16
-// stacks (agree.hpp:53-93 for the pixels this workgroup owns; see SearchArgs)
-template <int WORDS, bool NODUPES, int RP, int FUSE = 0>
+// The VALU search is kept as an independent cross-check of the matrix-core search
+// (BICOS_SEARCH=valu; identical results).
+template <int WORDS, bool NODUPES, int RP>
 __global__ __launch_bounds__(512) void search16_kernel(SearchArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
 
@@ -405,28 +429,6 @@ __global__ __launch_bounds__(512) void search16_kernel(SearchArgs a) {
             }
     }
 
-    if constexpr (FUSE != 0) {
-        // agree for this lane's pixels: col1 = best is always in the row, so NXC runs for
-        // every non-duplicate pixel; threshold -> float disparity, corrmap NaN otherwise
-        using TIn = typename std::conditional<FUSE == 1, uint8_t, uint16_t>::type;
-        const TIn* s0 = (const TIn*)a.stack0 + (size_t)row * a.row_pitch;
-        const TIn* s1 = (const TIn*)a.stack1 + (size_t)row * a.row_pitch;
-        float* outf = a.out_f32 + (size_t)row * a.out_pitch;
-        float* corr = a.corr ? a.corr + (size_t)row * a.out_pitch : nullptr;
-        int c0[R], best[R];
-        bool in[R], live[R];
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-            c0[r] = col0_base + r * 64;
-            best[r] = (int)(glo[r] & 0xFFFFu);
-            const bool dup = NODUPES && (int)(0xFFFFu - (ghi[r] & 0xFFFFu)) != best[r];
-            in[r] = c0[r] < cols;
-            live[r] = in[r] && !dup;
-        }
-        nxc::agree_pixels<TIn, R>(s0, s1, a.plane_pitch, a.n, c0, best, in, live, a.threshold,
-                                  a.has_minvar, a.minvar, outf, corr);
-        return;
-    }
     int16_t* __restrict__ out = a.out + (size_t)row * a.out_pitch;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
@@ -441,232 +443,6 @@ __global__ __launch_bounds__(512) void search16_kernel(SearchArgs a) {
             v = dup ? (int16_t)-1 : (int16_t)first;
         out[c0] = v;
     }
-}
-
-// Minimum over the 64 lanes of a wave, in lane 63 (DPP: row_shr 1/2/4/8 then the two
-// row broadcasts; lanes without a source keep their value, min is idempotent).
-__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x111, 0xF, 0xF, false));
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x112, 0xF, 0xF, false));
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x114, 0xF, 0xF, false));
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x118, 0xF, 0xF, false));
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x142, 0xA, 0xF, false));
-    v = min(v, (uint32_t)__builtin_amdgcn_update_dpp(-1, (int)v, 0x143, 0xC, 0xF, false));
-    return v;
-}
-
-// Fused forward + reverse search for Variant::Consistency (bicos.hpp:91-107).
-// The reverse search from col1 = best, bicos_search(drow1[best], drow0, cols), is the argmin
-// over col0 of column `best` of the same cost matrix (ham is symmetric), with the same
-// tie rule (lowest col0) and the same NoDuplicates rule. So one pass over the pairs yields
-// both: the row minima exactly as search16_kernel (forward), and the column minima of
-// this workgroup's col0 range for every col1: per pair one v_lshl_or builds
-// (col1_local << 16 | cost << 8 | col0_local) from the seeded popcount sum, the lane's R
-// keys fold with v_min, a DPP reduction takes the wave minimum, and the scalar unit turns
-// it into a (cost << 16 | col0) key parked in lane col1 % 64 of a register; every 64 col1
-// one ds_min_u32 merges the wave's keys into the workgroup's column array in LDS. The
-// array is written per row stage to rev_first[row][tile][col1] (rev_last: highest col0 at
-// the minimum, NoDuplicates) and consistency_keys_kernel takes the minimum over tiles.
-// Costs ~30 % more than one search instead of 100 %.
-template <int WORDS, bool NODUPES, int RP>
-__global__ __launch_bounds__(512) void search_lr_kernel(SearchArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t lds[];
-
-    const int nwg = gridDim.x;
-    const int bid = blockIdx.x;
-    const int per_xcd = (nwg + 7) / 8;
-    int logical = (bid % 8) * per_xcd + bid / 8;
-    if (nwg % 8 != 0) logical = bid;
-    const int row = logical / a.tiles_per_row;
-    const int tile = logical % a.tiles_per_row;
-
-    constexpr int R = 2 * RP;
-    const int split = a.split;
-    const int groups = blockDim.x / 64 / split;
-    const int wave = threadIdx.x / 64;
-    const int group = wave / split;
-    const int seg = wave % split;
-    const int lane = threadIdx.x % 64;
-    const int cols = a.cols;
-    const int grp_base = tile * groups * 64 * R + group * 64 * R;
-    const int col0_base = grp_base + lane;
-    const bool idle = grp_base >= cols;  // no col0 of this wave in the image: stage only
-    const uint32_t top_mask = WORDS == 8 ? 0x7FFFFFFFu : 0xFFFFFFFFu;
-
-    const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
-    const uint32_t* __restrict__ row1 = a.desc1 + (size_t)row * a.desc_pitch;
-
-    uint32_t d0[R][WORDS];
-    uint32_t glo[R], ghi[R];
-    uint32_t cfirst[R], clast[R];  // col0 in the column keys; all ones beyond the image
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int c0 = col0_base + r * 64;
-        const int cc = c0 < cols ? c0 : cols - 1;
-        lds_fetch<WORDS>(row0 + (size_t)cc * WORDS, d0[r]);
-        d0[r][WORDS - 1] &= top_mask;
-        glo[r] = 0xFFFFFFFFu;
-        ghi[r] = 0xFFFFFFFFu;
-        cfirst[r] = c0 < cols ? (uint32_t)(r * 64 + lane) : 0xFFFFFFFFu;
-        clast[r] = c0 < cols ? (uint32_t)(255 - (r * 64 + lane)) : 0xFFFFFFFFu;
-    }
-
-    uint32_t* colmin = lds + ((a.chunk * WORDS + 3) & ~3);  // [chunk] first, [chunk] last
-    const size_t rev_row = ((size_t)row * a.tiles_per_row + tile) * (size_t)cols;
-
-    for (int base = 0; base < cols; base += a.chunk) {
-        const int ncols = min(a.chunk, cols - base);
-        const int nwords = ncols * WORDS;
-        if (base) __syncthreads();
-        {
-            const uint32_t* src = row1 + (size_t)base * WORDS;
-            const int n4 = nwords / 4;
-            for (int i = threadIdx.x; i < n4; i += blockDim.x) {
-                uint4 v = ((const uint4*)src)[i];
-                if (WORDS == 8 && (i & 1)) v.w &= top_mask;
-                ((uint4*)lds)[i] = v;
-            }
-            for (int i = n4 * 4 + threadIdx.x; i < nwords; i += blockDim.x) lds[i] = src[i];
-            for (int i = threadIdx.x; i < ncols * (NODUPES ? 2 : 1); i += blockDim.x)
-                colmin[i] = 0xFFFFFFFFu;
-        }
-        __syncthreads();
-
-        for (int t0 = idle ? ncols : seg * 256; t0 < ncols; t0 += 256 * split) {
-            const int tn = min(256, ncols - t0);
-            uint32_t lo[RP], hi[RP];
-#pragma unroll
-            for (int p = 0; p < RP; ++p) {
-                lo[p] = 0xFFFFFFFFu;
-                hi[p] = 0xFFFFFFFFu;
-            }
-            const uint32_t* tl = lds + t0 * WORDS;
-            for (int jb = 0; jb < tn; jb += 64) {
-                const int jn = min(64, tn - jb);
-                uint32_t park_f = 0xFFFFFFFFu, park_l = 0xFFFFFFFFu;
-                auto step = [&](int j) {
-                    uint32_t d1[WORDS];
-                    lds_fetch<WORDS>(tl + j * WORDS, d1);
-                    const uint32_t seed = (uint32_t)j << 8;
-                    uint32_t cf = 0xFFFFFFFFu, cl = 0xFFFFFFFFu;
-#pragma unroll
-                    for (int p = 0; p < RP; ++p) {
-                        const uint32_t r0 = ham_seeded<WORDS>(d0[2 * p], d1, seed);
-                        const uint32_t r1 = ham_seeded<WORDS>(d0[2 * p + 1], d1, seed);
-                        const uint32_t key = __builtin_amdgcn_perm(r1, r0, 0x04050001u);
-                        lo[p] = pk_min_u16(lo[p], key);
-                        if (NODUPES) hi[p] = pk_min_u16(hi[p], key ^ 0x00FF00FFu);
-                        // (j << 16 | cost << 8 | col0_local): j is the same in every lane
-                        cf = min(cf, min((r0 << 8) | cfirst[2 * p], (r1 << 8) | cfirst[2 * p + 1]));
-                        if (NODUPES)
-                            cl = min(cl, min((r0 << 8) | clast[2 * p], (r1 << 8) | clast[2 * p + 1]));
-                    }
-                    const uint32_t sf = __builtin_amdgcn_readlane(wave_min_u32(cf), 63);
-                    const uint32_t kf = sf == 0xFFFFFFFFu ? sf
-                                        : (((sf >> 8) & 0xFFu) << 16) | ((uint32_t)grp_base + (sf & 0xFFu));
-                    park_f = lane == (j & 63) ? kf : park_f;
-                    if (NODUPES) {
-                        const uint32_t sl = __builtin_amdgcn_readlane(wave_min_u32(cl), 63);
-                        const uint32_t c0 = (uint32_t)grp_base + 255u - (sl & 0xFFu);
-                        const uint32_t kl = sl == 0xFFFFFFFFu ? sl
-                                            : (((sl >> 8) & 0xFFu) << 16) | (0xFFFFu - c0);
-                        park_l = lane == (j & 63) ? kl : park_l;
-                    }
-                };
-                constexpr int U = WORDS >= 8 ? 4 : 8;
-                int j = jb;
-                for (; j + U <= jb + jn; j += U) {
-#pragma unroll
-                    for (int u = 0; u < U; ++u) step(j + u);
-                }
-                for (; j < jb + jn; ++j) step(j);
-                if (lane < jn) {
-                    atomicMin(&colmin[t0 + jb + lane], park_f);
-                    if (NODUPES) atomicMin(&colmin[ncols + t0 + jb + lane], park_l);
-                }
-            }
-
-            // fold the tile's 16-bit keys into 32-bit (cost << 16 | col1) keys
-            const uint32_t tb = (uint32_t)(base + t0);
-#pragma unroll
-            for (int p = 0; p < RP; ++p) {
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const uint32_t v = (lo[p] >> (16 * h)) & 0xFFFFu;
-                    const uint32_t k = ((v >> 8) << 16) | (tb + (v & 0xFFu));
-                    glo[2 * p + h] = min(glo[2 * p + h], k);
-                    if (NODUPES) {
-                        const uint32_t w = (hi[p] >> (16 * h)) & 0xFFFFu;
-                        const uint32_t last = tb + 255u - (w & 0xFFu);
-                        const uint32_t kh = ((w >> 8) << 16) | (0xFFFFu - last);
-                        ghi[2 * p + h] = min(ghi[2 * p + h], kh);
-                    }
-                }
-            }
-        }
-        // this stage's column minima of the workgroup's col0 range -> global
-        __syncthreads();
-        for (int i = threadIdx.x; i < ncols; i += blockDim.x) {
-            a.rev_first[rev_row + base + i] = colmin[i];
-            if (NODUPES) a.rev_last[rev_row + base + i] = colmin[ncols + i];
-        }
-    }
-
-    if (split > 1) {
-        // merge the segments' forward minima (min of disjoint col1 ranges is exact)
-        __syncthreads();
-        uint32_t* m = lds;  // the row stage is dead now
-        const int slot = (group * 64 + lane) * R;
-        if (seg > 0) {
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                m[((seg - 1) * groups * 64 * R + slot + r) * 2] = glo[r];
-                m[((seg - 1) * groups * 64 * R + slot + r) * 2 + 1] = ghi[r];
-            }
-        }
-        __syncthreads();
-        if (seg > 0) return;
-        for (int q = 0; q < split - 1; ++q)
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                glo[r] = min(glo[r], m[(q * groups * 64 * R + slot + r) * 2]);
-                ghi[r] = min(ghi[r], m[(q * groups * 64 * R + slot + r) * 2 + 1]);
-            }
-    }
-
-    int16_t* __restrict__ out = a.out + (size_t)row * a.out_pitch;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        const int c0 = col0_base + r * 64;
-        if (c0 >= cols) continue;
-        const int first = (int)(glo[r] & 0xFFFFu);
-        const bool dup = NODUPES && (int)(0xFFFFu - (ghi[r] & 0xFFFFu)) != first;
-        out[c0] = dup ? (int16_t)-1 : (int16_t)first;  // forward best col1 (out_mode 1)
-    }
-}
-
-// Consistency from the fused search: fwd[c0] = best col1 (or -1); the reverse search of
-// col1 is the minimum over the row's col0 tiles of rev_first (lowest col0 at the minimum
-// cost) and, with NoDuplicates, rev_last (highest); bicos.hpp:99-106 otherwise.
-__global__ __launch_bounds__(256) void consistency_keys_kernel(ConsistencyArgs a) {
-    const int col = blockIdx.x * 256 + threadIdx.x;
-    const int row = blockIdx.y;
-    if (col >= a.cols) return;
-    const int16_t f = a.fwd[(size_t)row * a.cols + col];
-    int16_t v = INVALID_I16;
-    if (f >= 0) {
-        uint32_t first = 0xFFFFFFFFu, last = 0xFFFFFFFFu;
-        for (int t = 0; t < a.rev_tiles; ++t) {
-            const size_t o = ((size_t)row * a.rev_tiles + t) * (size_t)a.cols + f;
-            first = min(first, a.rev_first[o]);
-            if (a.rev_last) last = min(last, a.rev_last[o]);
-        }
-        const int rv = (int)(first & 0xFFFFu);
-        const bool dup = a.rev_last && (int)(0xFFFFu - (last & 0xFFFFu)) != rv;
-        if (first != 0xFFFFFFFFu && !dup && abs(col - rv) <= a.max_lr_diff)
-            v = (int16_t)((col + rv) / 2 - f);
-    }
-    a.out[(size_t)row * a.out_pitch + col] = v;
 }
 
 // Left-right consistency (bicos.hpp:99-106): fwd[c0] = best col1 (or -1), rev[c1] = best
@@ -897,9 +673,36 @@ hipError_t launch_tl(const TransformArgs& a, dim3 grid, hipStream_t st) {
     return hipGetLastError();
 }
 
+template <int WORDS, int MAXN>
+hipError_t launch_tl4(const TransformArgs& a, hipStream_t st) {
+    dim3 grid((a.cols / 4 + 255) / 256, a.rows, a.stack1 ? 2 : 1);
+    if (a.n == MAXN)
+        hipLaunchKernelGGL((transform4_kernel<WORDS, MAXN, true>), grid, dim3(256), 0, st, a);
+    else
+        hipLaunchKernelGGL((transform4_kernel<WORDS, MAXN, false>), grid, dim3(256), 0, st, a);
+    return hipGetLastError();
+}
+
+// u8 LIMITED with every dword load inside its row: 4 pixels per lane
+inline bool transform4_ok(const TransformArgs& a) {
+    const uintptr_t base = (uintptr_t)a.stack0 | (uintptr_t)(a.stack1 ? a.stack1 : a.stack0);
+    return a.cols % 4 == 0 && a.row_pitch % 4 == 0 && a.plane_pitch % 4 == 0 && base % 4 == 0;
+}
+
 template <typename TIn, int WORDS>
 hipError_t launch_transform_w(const TransformArgs& a, int mode, hipStream_t st) {
     dim3 grid((a.cols + 255) / 256, a.rows, a.stack1 ? 2 : 1);
+    if (sizeof(TIn) == 1 && mode == 0 && transform4_ok(a)) {
+        const int n = a.n;
+        if constexpr (WORDS == 1) return launch_tl4<WORDS, 9>(a, st);
+        else if constexpr (WORDS == 2) return n <= 12 ? launch_tl4<WORDS, 12>(a, st)
+                                                      : launch_tl4<WORDS, 17>(a, st);
+        else if constexpr (WORDS == 4) return n <= 24 ? launch_tl4<WORDS, 24>(a, st)
+                                                      : launch_tl4<WORDS, 33>(a, st);
+        else if (n <= 40) return launch_tl4<WORDS, 40>(a, st);
+        else if (n <= 48) return launch_tl4<WORDS, 48>(a, st);
+        else return launch_tl4<WORDS, 65>(a, st);
+    }
     if (mode == 0) {
         // descriptor width bounds n: 32 bits -> n <= 9, 64 -> 17, 128 -> 33, 256 -> 65
         const int n = a.n;
@@ -933,18 +736,6 @@ hipError_t launch_search16_r(const SearchArgs& a, int waves, hipStream_t st) {
     const size_t merge = a.split > 1 ? (size_t)(waves / a.split) * 64 * (2 * RP) * 8 * (a.split - 1) : 0;
     const size_t lds = stage > merge ? stage : merge;
     const int nwg = a.rows * a.tiles_per_row;
-    if constexpr (NODUPES) {
-        if (a.out_f32) {
-            if (a.depth == 1)
-                hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP, 1>), dim3(nwg),
-                                   dim3(64 * waves), lds, st, a);
-            else
-                hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP, 2>), dim3(nwg),
-                                   dim3(64 * waves), lds, st, a);
-            return hipGetLastError();
-        }
-    }
-    if (a.out_f32) return hipErrorInvalidValue;  // fused agree: NoDuplicates only
     hipLaunchKernelGGL((search16_kernel<WORDS, NODUPES, RP>), dim3(nwg), dim3(64 * waves), lds, st, a);
     return hipGetLastError();
 }
@@ -968,15 +759,11 @@ hipError_t launch_search_w(const SearchArgs& a, bool nodupes, const SearchGeomet
 template <typename TIn, typename TPrec, int MAXN>
 hipError_t launch_agree_m(const AgreeArgs& a, hipStream_t st) {
     dim3 grid((a.cols + 255) / 256, a.rows);
-    // left tile through LDS when the dword loads are aligned (BICOS_AGREE=reg: never)
-    static const bool reg_env = [] {
-        const char* v = std::getenv("BICOS_AGREE");
-        return v && !std::strcmp(v, "reg");
-    }();
+    // left tile through LDS when the dword loads are aligned
     const size_t sz = sizeof(TIn);
     const bool aligned = ((uintptr_t)a.stack0 % 4 == 0) && (a.row_pitch * sz) % 4 == 0 &&
                          (a.plane_pitch * sz) % 4 == 0;
-    if (aligned && !reg_env) {
+    if (aligned) {
         // runtime n even for an exact bucket: with a constant n the compiler front-loads
         // the conversions and doubles the VGPRs (49 -> 100 at n = 33)
         hipLaunchKernelGGL((agree_lds_kernel<TIn, TPrec, MAXN, false>), grid, dim3(256), 0, st, a);
@@ -1067,8 +854,6 @@ hipError_t launch_search(SearchArgs a, const SearchGeometry& g, int words, bool 
     a.tiles_per_row = g.tiles_per_row;
     a.split = g.split;
     if (g.waves % g.split) return hipErrorInvalidValue;
-    if (a.out_f32 && (!nodupes || (a.depth != 1 && a.depth != 2)))
-        return hipErrorInvalidValue;  // the fused agree epilogue exists for these only
     switch (words) {
         case 1: return launch_search_w<1>(a, nodupes, g, st);
         case 2: return launch_search_w<2>(a, nodupes, g, st);
@@ -1076,64 +861,6 @@ hipError_t launch_search(SearchArgs a, const SearchGeometry& g, int words, bool 
         case 8: return launch_search_w<8>(a, nodupes, g, st);
     }
     return hipErrorInvalidValue;
-}
-
-template <int WORDS, bool NODUPES, int RP>
-hipError_t launch_search_lr_r(const SearchArgs& a, int waves, hipStream_t st) {
-    const size_t stage = (size_t)((a.chunk * WORDS + 3) & ~3) * 4 +
-                         (size_t)a.chunk * 4 * (NODUPES ? 2 : 1);
-    const size_t merge = a.split > 1 ? (size_t)(waves / a.split) * 64 * (2 * RP) * 8 * (a.split - 1) : 0;
-    const size_t lds = stage > merge ? stage : merge;
-    const auto kern = search_lr_kernel<WORDS, NODUPES, RP>;
-    if (lds > 64 * 1024) {
-        const hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-    }
-    const int nwg = a.rows * a.tiles_per_row;
-    hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * waves), lds, st, a);
-    return hipGetLastError();
-}
-
-template <int WORDS, bool NODUPES>
-hipError_t launch_search_lr_n(const SearchArgs& a, const SearchGeometry& g, hipStream_t st) {
-    switch (g.R) {
-        case 2: return launch_search_lr_r<WORDS, NODUPES, 1>(a, g.waves, st);
-        case 4: return launch_search_lr_r<WORDS, NODUPES, 2>(a, g.waves, st);
-    }
-    return hipErrorInvalidValue;
-}
-
-template <int WORDS>
-hipError_t launch_search_lr_w(const SearchArgs& a, bool nodupes, const SearchGeometry& g,
-                              hipStream_t st) {
-    return nodupes ? launch_search_lr_n<WORDS, true>(a, g, st)
-                   : launch_search_lr_n<WORDS, false>(a, g, st);
-}
-
-hipError_t launch_search_lr(SearchArgs a, const SearchGeometry& g, int words, bool nodupes,
-                            hipStream_t st) {
-    if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
-    if (!a.rev_first || (nodupes && !a.rev_last)) return hipErrorInvalidValue;
-    a.chunk = g.chunk;
-    a.tiles_per_row = g.tiles_per_row;
-    a.split = g.split;
-    if (g.waves % g.split) return hipErrorInvalidValue;
-    switch (words) {
-        case 1: return launch_search_lr_w<1>(a, nodupes, g, st);
-        case 2: return launch_search_lr_w<2>(a, nodupes, g, st);
-        case 4: return launch_search_lr_w<4>(a, nodupes, g, st);
-        case 8: return launch_search_lr_w<8>(a, nodupes, g, st);
-    }
-    return hipErrorInvalidValue;
-}
-
-hipError_t launch_consistency_keys(const ConsistencyArgs& a, hipStream_t st) {
-    if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
-    if (!a.rev_first || a.rev_tiles < 1) return hipErrorInvalidValue;
-    dim3 grid((a.cols + 255) / 256, a.rows);
-    hipLaunchKernelGGL(consistency_keys_kernel, grid, dim3(256), 0, st, a);
-    return hipGetLastError();
 }
 
 hipError_t launch_consistency(const ConsistencyArgs& a, hipStream_t st) {

@@ -32,27 +32,6 @@ struct SearchArgs {
     int chunk;              // set by launch_search
     int tiles_per_row;      // set by launch_search
     int split;              // set by launch_search: waves per col0 group scanning col1 tiles
-    // fused Consistency (launch_search_lr): per-tile column minima [rows][tiles][cols]
-    uint32_t* rev_first = nullptr;
-    uint32_t* rev_last = nullptr;  // NoDuplicates only
-    // fused NXC agree (launch_search with out_f32 set; NoDuplicates search, no subpixel,
-    // single precision): the epilogue correlates each pixel with its best match and
-    // writes the float disparity (-32768 invalid) and the corrmap instead of `out`
-    float* out_f32 = nullptr;
-    float* corr = nullptr;          // may be null
-    const void* stack0 = nullptr;
-    const void* stack1 = nullptr;
-    int n = 0, depth = 0;
-    size_t row_pitch = 0, plane_pitch = 0;
-    float threshold = 0.f;
-    int has_minvar = 0;
-    float minvar = 0.f;             // already scaled by n
-    // fused transform -> search (launch_search_mx; LIMITED, <= 128-bit descriptors, the
-    // NoDuplicates any-order search): desc0/desc1 unused, descriptors computed from
-    // stack0/stack1 (n, depth, row_pitch, plane_pitch above)
-    int fused_tf = 0;
-    uint32_t tf_magic = 0;          // ceil(2^32 / n)
-    uint32_t stack_bytes = 0;       // bytes addressable from each stack base
 };
 
 struct SearchGeometry {
@@ -71,10 +50,6 @@ struct ConsistencyArgs {
     int rows, cols;
     size_t out_pitch;
     int max_lr_diff;
-    // fused search (consistency_keys_kernel): per-tile column minima instead of `rev`
-    const uint32_t* rev_first = nullptr;
-    const uint32_t* rev_last = nullptr;
-    int rev_tiles = 0;
 };
 
 struct AgreeArgs {
@@ -102,12 +77,6 @@ SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes,
 hipError_t launch_search(SearchArgs a, const SearchGeometry& g, int words, bool nodupes,
                          hipStream_t st);
 hipError_t launch_consistency(const ConsistencyArgs& a, hipStream_t st);
-// Fused forward + reverse search (Consistency): a.out gets the forward best col1 (or -1),
-// a.rev_first / a.rev_last [rows][g.tiles_per_row][cols] the column minima; g from
-// search_geometry(..., extra_col_bytes = 4 * (1 + nodupes)).
-hipError_t launch_search_lr(SearchArgs a, const SearchGeometry& g, int words, bool nodupes,
-                            hipStream_t st);
-hipError_t launch_consistency_keys(const ConsistencyArgs& a, hipStream_t st);
 
 // Matrix-core search (search_mx.hip): FP4 MFMA Hamming products, argmin keys in the
 // accumulator. Same outputs as launch_search (a.out, a.out_mode); no fused agree.

@@ -30,8 +30,6 @@
 // ds_read_b128 per lane. Accumulator map (32x32 shapes): lane l, register r holds row
 // (r & 3) + 8 (r >> 2) + 4 (l >> 5) (= col1 in the block) and column l & 31 (= col0).
 #include "kernels.hpp"
-#include "nxc.hpp"
-#include "transform.hpp"
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -39,24 +37,6 @@
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
-
-// 1: KEYS 2 reduces tiles in pairs (one lane-half exchange per two tiles); 0: per tile
-// (A/B builds, tools/build_alt.sh)
-#ifndef BICOS_MX_PAIRS
-#define BICOS_MX_PAIRS 1
-#endif
-// 1: KEYS 2 with 2 tiles per wave runs the software-pipelined block loop
-#ifndef BICOS_MX_PIPE
-#define BICOS_MX_PIPE 1
-#endif
-// 1: XK searches prefetch the next block's A fragments (block_pf)
-#ifndef BICOS_MX_PREFETCH
-#define BICOS_MX_PREFETCH 1
-#endif
-// 1: FK (KEYS 3) searches prefetch too
-#ifndef BICOS_MX_FK_PF
-#define BICOS_MX_FK_PF 0
-#endif
 
 namespace bicos_hip {
 
@@ -207,8 +187,6 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 //           matter (NoDuplicates, cols <= 8160; see below);
 //       3 = FK float keys, column in the free K half, ascending, no NoDuplicates
 //           (cols <= 2048, see FK_EPS).
-// FUSE: 0 = int16 `out`; 1 / 2 = NXC agree fused into the epilogue on u8 / u16 stacks
-// (agree.hpp:53-93 for the pixels the lane owns; float disparity + corrmap, see SearchArgs).
 //
 // KEYS 2. NoDuplicates needs the LAST column at the minimum cost only to compare it with
 // the first; a block none of whose keys reaches the running minimum cost cannot hold it. So
@@ -222,22 +200,11 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 // blocks still do it). The result is exact whatever the data: the order only changes speed.
 // Keys stay relative to the base B of the block being reduced (shifts by the signed
 // B - B_prev); C = 768 + (8160 + col1 % 32) * 2^-14 keeps both fields in [0, 16383].
-// TF: 0 = descriptors from desc0 / desc1; 1 / 2 = fused transform -> search on u8 / u16
-// stacks (LIMITED): the left descriptors of the wave's tiles and the right row's, chunk by
-// chunk, are computed from the stacks (transform.hpp) instead of read from HBM
-template <int TIn_bytes>
-struct tf_type { using type = uint8_t; };
-template <>
-struct tf_type<2> { using type = uint16_t; };
-constexpr int tf_maxn(int words) { return words == 1 ? 9 : words == 2 ? 17 : 33; }
-
-template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, int FUSE = 0, int TF = 0>
+template <int WORDS, int KSU, bool NODUPES, int T, int KEYS>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void search_mx_kernel(SearchArgs a) {
-    static_assert(TF == 0 || WORDS <= 4, "fused transform: descriptors up to 128 bits");
-    using TTF = typename tf_type<TF == 2 ? 2 : 1>::type;
     constexpr bool FK = KEYS == 3;
-    static_assert(!FK || (!NODUPES && FUSE == 0 && TF == 0), "FK keys: first minimum only");
+    static_assert(!FK || !NODUPES, "FK keys: first minimum only");
     constexpr bool XK = KEYS == 1 || KEYS == 2;
     constexpr bool FREE = KEYS == 2;
     static_assert(!FREE || NODUPES, "KEYS 2 is the NoDuplicates search");
@@ -278,27 +245,11 @@ void search_mx_kernel(SearchArgs a) {
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const int c0 = c0_wave + 32 * t + j;
-        uint32_t wl[WORDS];  // TF: the pixel's descriptor, computed from the left stack
-        if constexpr (TF != 0) {
-#pragma unroll
-            for (int q = 0; q < WORDS; ++q) wl[q] = 0;
-            if (c0 < cols)
-                limited_descriptor<TTF, WORDS, tf_maxn(WORDS), false>(
-                    StackReader<TTF>(a.stack0, a.stack_bytes), (uint32_t)c0,
-                    (uint32_t)row * (uint32_t)a.row_pitch, (uint32_t)a.plane_pitch, a.n, a.tf_magic, wl);
-        }
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const int w = 2 * s + h;
             uint32_t x = 0;
-            if constexpr (TF != 0) {
-                // word 2s + h: a select of the two static slots (no dynamic register index)
-                const uint32_t lo = 2 * s < WORDS ? wl[(2 * s) % WORDS] : 0u;
-                const uint32_t hi = 2 * s + 1 < WORDS ? wl[(2 * s + 1) % WORDS] : 0u;
-                x = h ? hi : lo;
-            } else {
-                if (c0 < cols && w < WORDS) x = row0[(size_t)c0 * WORDS + w];
-            }
+            if (c0 < cols && w < WORDS) x = row0[(size_t)c0 * WORDS + w];
             if (WORDS == 8 && KS == 4 && w == 7) x &= 0x7FFFFFFFu;  // bit 255 masked (see below)
             bf[t][s] = expand_bits(x, LUT_B);
         }
@@ -306,15 +257,15 @@ void search_mx_kernel(SearchArgs a) {
 
     // PAIRS (KEYS 2): the running first minima of tiles 2p / 2p+1 share register mp[p]
     // (lanes 0-31 / 32-63: the halves that write those tiles), see block()
-    constexpr bool PAIRS = FREE && T % 2 == 0 && BICOS_MX_PAIRS;
+    constexpr bool PAIRS = FREE && T % 2 == 0;
     // one pair per wave: the block loop is software-pipelined (see the FREE chunk loop)
-    constexpr bool PIPE = PAIRS && T == 2 && BICOS_MX_PIPE;
+    constexpr bool PIPE = PAIRS && T == 2;
     // XK full blocks: the next block's A fragments are read while this one is reduced.
     // Only where the registers allow (paired NoDuplicates tiles, <= 2 K-steps): cfg2 -1.5 %,
     // cfg5 -1 %; with 3 K-steps the extra live fragments spill inside the loop (cfg4 2.3x
     // slower)
-    // (FK: the registers of the C matrix pay for the prefetched fragments at 3 K-steps)
-    constexpr bool PREFETCH = ((XK && PAIRS && KS <= 2) || (FK && BICOS_MX_FK_PF)) && BICOS_MX_PREFETCH;
+    // (FK at 3 K-steps: 25 registers spill even with the C matrix gone)
+    constexpr bool PREFETCH = XK && PAIRS && KS <= 2;
     uint32_t m1[T], m2[T], mp[T / 2 > 0 ? T / 2 : 1];
     int b2[T];  // KEYS 2: the base m2[t] is relative to (wave-uniform)
 #pragma unroll
@@ -444,23 +395,10 @@ void search_mx_kernel(SearchArgs a) {
         // expand the chunk's right descriptors: one col1 per thread, all its words
         for (int c = threadIdx.x; expand && c < chunk; c += blockDim.x) {
             const int c1 = base + c;
-            uint32_t wr[WORDS];  // TF: the right pixel's descriptor from the right stack
-            if constexpr (TF != 0) {
-#pragma unroll
-                for (int q = 0; q < WORDS; ++q) wr[q] = 0;
-                if (c1 < cols)
-                    limited_descriptor<TTF, WORDS, tf_maxn(WORDS), false>(
-                        StackReader<TTF>(a.stack1, a.stack_bytes), (uint32_t)c1,
-                        (uint32_t)row * (uint32_t)a.row_pitch, (uint32_t)a.plane_pitch, a.n, a.tf_magic, wr);
-            }
 #pragma unroll
             for (int w = 0; w < WL; ++w) {
                 uint32_t x = 0;
-                if constexpr (TF != 0) {
-                    x = w < WORDS ? wr[w % WORDS] : 0u;
-                } else {
-                    if (c1 < cols && w < WORDS) x = row1[(size_t)c1 * WORDS + w];
-                }
+                if (c1 < cols && w < WORDS) x = row1[(size_t)c1 * WORDS + w];
                 if (WORDS == 8 && KS == 4 && w == 7) x &= 0x7FFFFFFFu;
                 if (FK && w == WL - 1)  // (the descriptors leave this slot 0: host check)
                     lds_mx[w * chunk + c] = fk_digits(c1 & 31);
@@ -672,31 +610,6 @@ void search_mx_kernel(SearchArgs a) {
         else if constexpr (NODUPES) return key_col(m2[t]) == best;
         return true;
     };
-    if constexpr (FUSE != 0) {
-        // half 0 owns the even tiles, half 1 the odd ones: T/2 pixels per lane, correlated
-        // together with their best match straight from the stacks (no int16 map, no agree
-        // launch); col1 = best is always inside the row
-        using TIn = typename std::conditional<FUSE == 1, uint8_t, uint16_t>::type;
-        constexpr int TH = T / 2;
-        int c0[TH], best[TH];
-        bool in[TH], live[TH];
-#pragma unroll
-        for (int i = 0; i < TH; ++i) {
-            const int b0 = best_of(2 * i), b1 = best_of(2 * i + 1);
-            const bool u0 = unique_of(2 * i, b0), u1 = unique_of(2 * i + 1, b1);
-            c0[i] = c0_wave + 32 * (2 * i + h) + j;
-            best[i] = h ? b1 : b0;
-            in[i] = c0[i] < cols;
-            live[i] = in[i] && (h ? u1 : u0);
-        }
-        const TIn* s0 = (const TIn*)a.stack0 + (size_t)row * a.row_pitch;
-        const TIn* s1 = (const TIn*)a.stack1 + (size_t)row * a.row_pitch;
-        float* outf = a.out_f32 + (size_t)row * a.out_pitch;
-        float* corr = a.corr ? a.corr + (size_t)row * a.out_pitch : nullptr;
-        nxc::agree_pixels<TIn, TH>(s0, s1, a.plane_pitch, a.n, c0, best, in, live, a.threshold,
-                                   a.has_minvar, a.minvar, outf, corr);
-        return;
-    }
     int16_t* out = a.out + (size_t)row * a.out_pitch;
     // (lane index made opaque: otherwise the compiler hoists these addresses into the
     // prologue, where they share c0 with the B-fragment loads, and spills them to scratch
@@ -723,24 +636,7 @@ template <int WORDS, int KSU, bool NODUPES, int T, int KEYS>
 hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     constexpr int WL = 2 * KSU;
     const size_t lds = (size_t)WL * a.chunk * 16;
-    // fused agree only with the NoDuplicates search (the pipeline's)
-    auto pick = [&]() {
-        if constexpr (NODUPES) {
-            if (a.out_f32) return a.depth == 2 ? search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 2>
-                                               : search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 1>;
-        }
-        if constexpr (KEYS == 2 && WORDS <= 4) {
-            if (a.fused_tf) return a.depth == 2 ? search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 0, 2>
-                                                : search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 0, 1>;
-        }
-        return search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, 0>;
-    };
-    // the fused transform: the NoDuplicates any-order search (KEYS 2), up to 128 bits,
-    // u8 / u16 stacks, not with the fused agree
-    if (a.fused_tf && (KEYS != 2 || WORDS > 4 || a.out_f32 || (a.depth != 1 && a.depth != 2)))
-        return hipErrorInvalidValue;
-    if (a.out_f32 && (!NODUPES || (a.depth != 1 && a.depth != 2))) return hipErrorInvalidValue;
-    const auto kern = pick();
+    const auto kern = search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -778,18 +674,14 @@ hipError_t launch_mx_k(const SearchArgs& a, const MxGeometry& g, hipStream_t st)
 template <int WORDS, int KSU, bool NODUPES>
 hipError_t launch_mx_t(const SearchArgs& a, const MxGeometry& g, hipStream_t st) {
     // one-product XK keys by default: with NoDuplicates in any block order up to 8160
-    // columns (BICOS_MX_ORDER=natural: ascending), ascending up to 16384; the two-product
-    // float keys beyond that, or when tuned (variant 66)
-    static const bool natural = [] {
-        const char* v = std::getenv("BICOS_MX_ORDER");
-        return v && !std::strcmp(v, "natural");
-    }();
+    // columns, ascending up to 16384; the two-product float keys beyond that, or when tuned
+    // (variant 66)
     if (g.keys == 1) {
         if constexpr (!NODUPES) {
             if (g.fk) return launch_mx_k<WORDS, KSU, NODUPES, 3>(a, g, st);
         }
         if constexpr (NODUPES) {
-            if (a.cols <= XKF_MAX_COLS && !natural) return launch_mx_k<WORDS, KSU, NODUPES, 2>(a, g, st);
+            if (a.cols <= XKF_MAX_COLS) return launch_mx_k<WORDS, KSU, NODUPES, 2>(a, g, st);
         }
         if (a.cols <= 16384) return launch_mx_k<WORDS, KSU, NODUPES, 1>(a, g, st);
     }

@@ -6,8 +6,6 @@
 // SIMD, arrays past 256 registers) run the SLP build: subpixel_wide.hip.
 #include "subpixel.hpp"
 
-#include <cstdlib>
-
 namespace bicos_hip {
 
 namespace {
@@ -21,15 +19,6 @@ namespace {
 #ifndef BICOS_SP33_NCS
 #define BICOS_SP33_NCS 18
 #endif
-// BICOS_SUBPIXEL_STAGE=0: the register-only kernel (A/B)
-bool subpixel_stage() {
-    static const bool on = [] {
-        const char* v = std::getenv("BICOS_SUBPIXEL_STAGE");
-        return !(v && v[0] == '0');
-    }();
-    return on;
-}
-
 template <typename TIn, typename TPrec>
 hipError_t launch_subpixel_t(const AgreeArgs& a, int depth, bool dbl, hipStream_t st) {
     const int n = a.n;
@@ -37,10 +26,9 @@ hipError_t launch_subpixel_t(const AgreeArgs& a, int depth, bool dbl, hipStream_
     if (n <= 16) return launch_subpixel_m<TIn, TPrec, 16, 9>(a, st);
     if (n <= 24) return launch_subpixel_m<TIn, TPrec, 24, 17>(a, st);
     if (n <= 33) {
-        if constexpr (sizeof(TPrec) == 4) {
-            if (subpixel_stage()) return launch_subpixel_m<TIn, TPrec, 33, 25, BICOS_SP33_NCS, 3>(a, st);
-        }
-        return launch_subpixel_m<TIn, TPrec, 33, 25>(a, st);
+        // single precision: the LDS-staged kernel; double keeps every array in registers
+        if constexpr (sizeof(TPrec) == 4) return launch_subpixel_m<TIn, TPrec, 33, 25, BICOS_SP33_NCS, 3>(a, st);
+        else return launch_subpixel_m<TIn, TPrec, 33, 25>(a, st);
     }
     if (n <= 40) return launch_subpixel_m<TIn, TPrec, 40, 34>(a, st);
     return launch_subpixel_wide(a, depth, dbl, st);

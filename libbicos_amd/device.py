@@ -227,24 +227,6 @@ class Engine:
         return out, corr
 
 
-    def search_agree(self, desc0: torch.Tensor, desc1: torch.Tensor, stack0: torch.Tensor,
-                     stack1: torch.Tensor, words: int, threshold: float,
-                     minvar_scaled: Optional[float] = None, stream=None
-                     ) -> Tuple[torch.Tensor, torch.Tensor]:
-        """NoDuplicates search with the NXC agree fused into its epilogue
-        (bicos_search_agree_device) -> (float disparity, corrmap)."""
-        n, rows, cols, rp, pp = _check_stack(stack0)
-        out = torch.empty((rows, cols), dtype=torch.float32, device=stack0.device)
-        corr = torch.empty((rows, cols), dtype=torch.float32, device=stack0.device)
-        hm = int(minvar_scaled is not None)
-        rc = self._L.bicos_search_agree_device(
-            self._h, desc0.data_ptr(), desc1.data_ptr(), stack0.data_ptr(), stack1.data_ptr(), n,
-            rows, cols, rp, pp, _depth(stack0), words, threshold, hm, float(minvar_scaled or 0.0),
-            out.data_ptr(), corr.data_ptr(), _stream(stack0.device, stream))
-        _lib.check(rc, "bicos_search_agree_device")
-        return out, corr
-
-
 def used_bits(n: int, mode: int = 0) -> int:
     """Upper bound of the descriptor bits the transform sets (LIMITED 4n-6 for n >= 4, 7 for
     n = 3, 4 for n = 2 (descriptor_transform.hpp:62-68 alone); FULL n^2-2n+3; reference

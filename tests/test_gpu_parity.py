@@ -70,6 +70,34 @@ def test_transform_bit_exact(gpu, oracle, n, mode, dt):
     same(out[:, : 301 * words].reshape(13, 301, words), ref)
 
 
+# u8 LIMITED stacks whose width, pitches and bases are multiples of 4 take the four-pixels-
+# per-lane transform (kernels.hip transform4_kernel): every n bucket, exact and padded, on
+# random stacks with the extreme values 0 / 255 present, and on a plane-pitch-padded view
+@pytest.mark.parametrize("n", [2, 3, 4, 5, 8, 9, 10, 12, 16, 17, 23, 24, 25, 32, 33, 34, 40,
+                               41, 47, 48, 49, 64, 65])
+def test_transform4_bit_exact(gpu, oracle, n):
+    mode = 0
+    s = random_stack(n, 9, 324, np.uint8, seed=500 + n)
+    s[:, 0, :8] = 0
+    s[:, 1, :8] = 255
+    s[n // 2, 2, 4:12] = 255
+    words = oracle.desc_words(n, mode)
+    ref = oracle.transform(s, mode, words)
+    out = host(gpu.transform(dev(s), mode, words)).view(np.uint32)
+    same(out[:, : 324 * words].reshape(9, 324, words), ref)
+
+
+def test_transform4_padded_pitches(gpu, oracle):
+    import torch
+    n, H, W, P = 33, 11, 200, 256
+    s = random_stack(n, H, W, np.uint8, seed=77)
+    buf = torch.zeros((n, H + 3, P), dtype=torch.uint8, device="cuda")
+    buf[:, :H, :W] = dev(s)
+    words = oracle.desc_words(n, 0)
+    out = host(gpu.transform(buf[:, :H, :W], 0, words)).view(np.uint32)
+    same(out[:, : W * words].reshape(H, W, words), oracle.transform(s, 0, words))
+
+
 # -------------------------------------------------------------------- search
 def _low_entropy_desc(H, W, words, seed, bits=6):
     rng = np.random.default_rng(seed)
@@ -382,13 +410,13 @@ def test_empty_and_tiny(gpu, oracle):
         same(gpu_match(gpu, L, R, **cfg)[0], oracle.match(L, R, cfg_of(oracle, **cfg))[0])
 
 
-# Fused forward + reverse Consistency search (search_lr_kernel): rows wider than one LDS
-# stage (column minima flushed per stage), reverse duplicates (low-entropy stacks), every
-# register blocking / col1 split, and several col0 tiles per row.
+# Consistency on the VALU cross-check search (forward + full reverse search16_kernel): rows
+# wider than one LDS stage, reverse duplicates (low-entropy stacks), every register
+# blocking / col1 split, and several col0 tiles per row.
 @pytest.mark.parametrize("n,H,W,maxval", [(40, 3, 2600, None), (17, 5, 3000, None),
                                           (8, 6, 700, 3), (33, 4, 1100, 2)])
 @pytest.mark.parametrize("no_dupes", [False, True])
-def test_fused_consistency_edges(gpu, oracle, n, H, W, maxval, no_dupes):
+def test_valu_consistency_edges(gpu, oracle, n, H, W, maxval, no_dupes):
     if maxval is None:
         L, R = stereo_stack(n, H, W, dmin=4, drange=40, seed=n + W)
     else:
@@ -403,57 +431,6 @@ def test_fused_consistency_edges(gpu, oracle, n, H, W, maxval, no_dupes):
         finally:
             gpu.tune(0, 0, 0, 0)
         same(d, rd)
-
-
-# The NXC agree fused into the search epilogue (what match runs without Consistency /
-# subpixel / DOUBLE; search16_kernel or search_mx_kernel) == the search followed by the
-# separate agree kernel, byte for byte.
-@pytest.mark.parametrize("n,H,W,dt,minvar", [(8, 5, 700, np.uint8, None), (17, 4, 1300, np.uint16, 1.5),
-                                             (33, 6, 2048, np.uint8, 2.0), (40, 3, 900, np.uint8, None)])
-def test_fused_search_agree_equals_separate(gpu, n, H, W, dt, minvar):
-    from libbicos_amd.device import descriptor_words
-    L, R = stereo_stack(n, H, W, dt, dmin=3, drange=30, seed=n + W)
-    L[:, 1, 100:140] = 7  # flat patch: variance 0 -> NaN correlation / min-variance reject
-    s0, s1 = dev(L), dev(R)
-    words = descriptor_words(n, 0)
-    d0, d1 = gpu.transform(s0, 0, words), gpu.transform(s1, 0, words)
-    mv = None if minvar is None else float(np.float32(minvar) * np.float32(n))
-    # default (matrix cores), VALU variants, matrix-core key forms / tile counts / pipeline
-    for tune in [(0, 0, 0, 0), (16, 4, 8, 0), (16, 2, 8, 4), (65, 2, 8, 0), (65, 8, 4, 0),
-                 (66, 4, 8, 0), (64, 4, 8, 40)]:
-        gpu.tune(*tune)
-        try:
-            fo, fc = gpu.search_agree(d0, d1, s0, s1, words, 0.8, minvar_scaled=mv)
-            raw = gpu.search(d0, d1, W, words, 1)
-            so, sc = gpu.agree(raw, s0, s1, 0.8, mv)
-        finally:
-            gpu.tune(0, 0, 0, 0)
-        same(host(fo), host(so))
-        same(host(fc), host(sc))
-
-
-# The fused transform -> search (BICOS_FUSE_TRANSFORM=1: descriptors computed from the
-# stacks inside the matrix-core search) == the transform kernel +
-# search, byte for byte, for every descriptor width it covers (LIMITED, <= 128 bits), u8 /
-# u16, ragged widths, NXC / subpixel / no NXC; and the oracle on one case.
-@pytest.mark.parametrize("n,H,W,dt,kw", [
-    (2, 3, 40, np.uint8, {}), (8, 5, 700, np.uint8, dict(nxcorr_threshold=0.8)),
-    (9, 4, 333, np.uint16, dict(nxcorr_threshold=0.5, min_variance=1.0)),
-    (17, 4, 1300, np.uint16, dict(nxcorr_threshold=0.8)), (24, 3, 97, np.uint8, {}),
-    (33, 6, 2048, np.uint8, dict(nxcorr_threshold=0.96)),
-    (33, 4, 1030, np.uint8, dict(nxcorr_threshold=0.9, subpixel_step=0.25))])
-def test_fused_transform_search_equals_separate(gpu, oracle, n, H, W, dt, kw, monkeypatch):
-    L, R = stereo_stack(n, H, W, dt, dmin=3, drange=30, seed=n * 7 + W)
-    monkeypatch.setenv("BICOS_FUSE_TRANSFORM", "0")
-    d_ref, c_ref = gpu_match(gpu, L, R, **kw)
-    monkeypatch.setenv("BICOS_FUSE_TRANSFORM", "1")
-    d_f, c_f = gpu_match(gpu, L, R, **kw)
-    same(d_f, d_ref)
-    if c_ref is not None:
-        same(c_f, c_ref)
-    if n == 33 and W == 2048:
-        do, _ = oracle.match(L, R, cfg_of(oracle, **kw))
-        same(d_f, do)
 
 
 @pytest.mark.parametrize("n,H,W,dt,kw", [

@@ -28,7 +28,6 @@ for step in "$@"; do
         pytest) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ;;
         pytestk) run pytest_gpu 900 python -m pytest tests -m gpu -q ;;
         bench) run bench 600 python bench.py --steps 20 --warmup 3 ;;
-        benchnf) BICOS_FUSE_AGREE=0 run benchnf 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-path ;;
         benchf) run benchf 600 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-host-path ;;
         bench3) run bench3 600 python bench.py --config cfg3 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
         ab1|ab3|ab2|ab4)  # A/B on one box: current lib vs build/alt.so (same bench, interleaved twice)
@@ -80,8 +79,6 @@ for step in "$@"; do
             cp build/cur.so libbicos_amd/libbicos_amd.so ;;
         subpix16) run subpix16 300 python tools/subpix_bench.py --depth 2 --ns 8,16,24,33 ;;
         bench4) run bench4 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
-        bench4tp) BICOS_CONSISTENCY=twopass run bench4tp 600 python bench.py --config cfg4 --steps 10 --warmup 2 --no-cpu-baseline --no-host-path ;;
-        pytesttp) BICOS_CONSISTENCY=twopass run pytest_tp 900 python -m pytest tests -m gpu -x -q -k "consist or cons or cfg4 or golden or tuning" ;;
         stagekib)
             for c in cfg5 cfg4f; do for k in 0 40 32; do
                 BICOS_SEARCH_STAGE_KIB=$k run stage_${c}_$k 300 python bench.py --config $c --steps 8 --warmup 2 --no-cpu-baseline --no-host-path
@@ -92,7 +89,6 @@ for step in "$@"; do
         pmcclk) for c in ${CLKCFG:-cfg2 cfg4}; do
                 run pmcclk_$c 120 timeout -s KILL 100 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU -d gpurun_out/pmcclk_$c -o run --output-format csv -- python tools/search_sweep.py --config $c --rounds 1 --reps 3 --variants ${SV:-0:0:0}
             done ;;
-        sweepnat) BICOS_MX_ORDER=natural run sweepnat_${SC:-cfg2} 600 python tools/search_sweep.py --config ${SC:-cfg2} --variants $SV ;;
         diag)  # search-kernel floors: diagnostic builds (tools/build_diag.sh) vs the real one
             cp libbicos_amd/libbicos_amd.so build/cur.so
             run diag_real_${SC:-cfg2} 300 python tools/search_sweep.py --config ${SC:-cfg2} --variants ${SV:-0:0:0}
