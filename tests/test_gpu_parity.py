@@ -163,6 +163,34 @@ def test_agree_bit_exact(gpu, oracle, n, dt, minvar, W):
     same(host(corr), rc)
 
 
+# u8 stacks with 4-aligned widths run agree4_kernel (4 pixels per lane): flat disparity runs
+# (one v_perm from two aligned dwords), +-1/+-2 jitter inside a lane (still one 8-byte
+# window), jumps wider than the window (the wave falls back to byte loads), matches off
+# either edge of the row, invalid pixels, NaN correlations, int16 and float outputs
+@pytest.mark.parametrize("n", [2, 7, 8, 16, 24, 33, 40])
+@pytest.mark.parametrize("minvar", [None, 2.0])
+def test_agree4_window_paths(gpu, oracle, n, minvar):
+    H, W = 8, 1024
+    L, R = stereo_stack(n, H, W, np.uint8, dmin=3, drange=40, seed=n + 1000)
+    rng = np.random.default_rng(n)
+    raw = np.empty((H, W), np.int16)
+    raw[0] = 17                                              # flat
+    raw[1] = 20 + rng.integers(-1, 2, size=W)                # jitter within a lane
+    raw[2] = 30 + rng.integers(-2, 3, size=W)
+    raw[3] = np.where(np.arange(W) % 64 < 32, 5, 250)        # jumps wider than the window
+    raw[4] = rng.integers(-40, 1100, size=W)                 # anything, incl. off-row matches
+    raw[5] = 12
+    raw[5, ::7] = -32768                                     # invalid pixels in flat runs
+    raw[6] = np.arange(W) % 9 - 4                            # negative disparities (col1 > col0)
+    raw[7] = 1023                                            # col1 = col0 - 1023: only col 1023 in row
+    R[:, 0, 40:48] = 9                                       # flat right pixels: NaN correlations
+    mv = None if minvar is None else np.float32(minvar) * np.float32(n)
+    rd, rc = oracle.agree(raw, L, R, 0.5, mv)
+    out, corr = gpu.agree(dev(raw), dev(L), dev(R), 0.5, None if mv is None else float(mv))
+    same(host(out), rd.astype(np.float32))
+    same(host(corr), rc)
+
+
 # n covers exact buckets and padded ones (2, 12, 25, 45, 60: slots n..MAXN-1 are exact
 # no-ops) in both loop structures (pipelined MAXN <= 40, top-of-step above); steps cover
 # 41/20/8 x values, 3 and a single x (step > 2)
