@@ -199,31 +199,6 @@ __global__ __launch_bounds__(256) void transform_limited_kernel(TransformArgs a)
     }
 }
 
-// Four u8 pixels per lane (transform.hpp limited_descriptor4): one dword load per plane
-// instead of four byte loads; used for u8 LIMITED stacks whose columns, pitches and bases
-// are multiples of 4 (launch_transform), the one-pixel kernel above otherwise.
-template <int WORDS, int MAXN, bool EXACT>
-__global__ __launch_bounds__(256) void transform4_kernel(TransformArgs a) {
-    const int col4 = (blockIdx.x * 256 + threadIdx.x) * 4;
-    const int row = blockIdx.y;
-    const int which = blockIdx.z;
-    if (col4 >= a.cols) return;
-    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<void*>(which ? a.stack1 : a.stack0), (short)0, (int)a.stack_bytes, 0x00020000);
-    uint32_t* __restrict__ out = (which ? a.desc1 : a.desc0) + (size_t)row * a.desc_pitch + (size_t)col4 * WORDS;
-    uint32_t w[4][WORDS];
-    limited_descriptor4<WORDS, MAXN, EXACT>(r, (uint32_t)col4, (uint32_t)row * (uint32_t)a.row_pitch,
-                                            (uint32_t)a.plane_pitch, a.n, a.magic, w);
-    // the 4 pixels' 4 x WORDS words are contiguous and 16-byte aligned (desc_pitch % 4 == 0)
-#pragma unroll
-    for (int q = 0; q < WORDS; ++q) {
-        const int f = 4 * q;  // flat word index f .. f+3 of [pixel][word]
-        *(uint4*)(out + f) = make_uint4(w[f / WORDS][f % WORDS], w[(f + 1) / WORDS][(f + 1) % WORDS],
-                                        w[(f + 2) / WORDS][(f + 2) % WORDS],
-                                        w[(f + 3) / WORDS][(f + 3) % WORDS]);
-    }
-}
-
 // --------------------------------------------------------------------- search
 
 // Hamming cost of one (col0, col1) pair.
@@ -662,136 +637,6 @@ __global__ __launch_bounds__(256) void agree_lds_kernel(AgreeArgs a) {
 
 
 
-// agree for four u8 pixels per lane (single precision). The left samples of the lane's 4
-// columns are one dword per plane; the right samples of its 4 matches (col - d_k) lie in
-// the 8 bytes of two aligned dwords per plane whenever the 4 disparities differ by at most
-// 4 (always on a flat disparity run), and one v_perm_b32 per plane packs the 4 wanted bytes
-// into one dword -- 3 dword loads per plane for 4 pixels instead of 4 byte gathers + a
-// quarter dword. A wave any of whose lanes spreads wider takes per-pixel byte loads for
-// every plane (wave-uniform branch; same results). Sums in 16-bit lanes (pixels 0/2 and
-// 1/3 of a dword at once), then the reference's float arithmetic per pixel exactly as
-// agree_lds_kernel. Requires cols, pitches, stack bases and the maps 4-pixel aligned
-// (launch_agree_m checks; agree_lds_kernel otherwise).
-template <int MAXN>
-__global__ __launch_bounds__(256) void agree4_kernel(AgreeArgs a) {
-    int tile, row;
-    xcd_rows(tile, row);
-    const int col4 = (tile * 256 + (int)threadIdx.x) * 4;
-    if (col4 >= a.cols) return;
-    const int n = a.n;
-    const uint32_t pp = (uint32_t)a.plane_pitch;
-    const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
-    const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<void*>(a.stack0), (short)0, (int)a.stack_bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<void*>(a.stack1), (short)0, (int)a.stack_bytes, 0x00020000);
-    // the four disparities (one 8-byte load) and the left samples (independent of them)
-    const uint2 dd = *(const uint2*)(a.raw + (size_t)row * a.raw_pitch + col4);
-    int d[4] = {(int)(int16_t)(dd.x & 0xFFFFu), (int)(int16_t)(dd.x >> 16),
-                (int)(int16_t)(dd.y & 0xFFFFu), (int)(int16_t)(dd.y >> 16)};
-    uint32_t L[MAXN];
-#pragma unroll
-    for (int t = 0; t < MAXN; ++t)  // unconditional (slots past n: plane n-1, unused)
-        L[t] = __builtin_amdgcn_raw_buffer_load_b32(r0, (uint32_t)col4, rowoff + (uint32_t)min(t, n - 1) * pp, 0);
-    bool inb[4];
-    int pos[4];
-    int lo = 0x7FFFFFFF, hi = -1;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int c1 = col4 + k - d[k];
-        inb[k] = d[k] != INVALID_I16 && c1 >= 0 && c1 < a.cols;
-        pos[k] = c1;
-        if (inb[k]) {
-            lo = min(lo, c1);
-            hi = max(hi, c1);
-        }
-    }
-    if (hi < 0) lo = hi = col4;  // no match in the lane: any in-row window
-    const int base = lo & ~3;
-    const bool narrow = hi - base < 8;
-    uint32_t sel = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) sel |= (uint32_t)((inb[k] ? pos[k] : lo) - base) << (8 * k);
-    uint32_t R[MAXN];
-    if (__builtin_amdgcn_ballot_w64(!narrow) == 0) {
-        // two aligned dwords per plane hold all 4 samples; pick them with one v_perm
-        // (selector bytes 0..3 = the first dword's bytes, 4..7 = the second's)
-#pragma unroll
-        for (int t = 0; t < MAXN; ++t) {
-            const uint32_t off = rowoff + (uint32_t)min(t, n - 1) * pp;
-            const uint32_t w0 = __builtin_amdgcn_raw_buffer_load_b32(r1, (uint32_t)base, off, 0);
-            const uint32_t w1 = __builtin_amdgcn_raw_buffer_load_b32(r1, (uint32_t)base + 4u, off, 0);
-            R[t] = __builtin_amdgcn_perm(w1, w0, sel);
-        }
-    } else {
-#pragma unroll
-        for (int t = 0; t < MAXN; ++t) {
-            const uint32_t off = rowoff + (uint32_t)min(t, n - 1) * pp;
-            uint32_t v = 0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                v |= __builtin_amdgcn_raw_buffer_load_b8(r1, (uint32_t)(inb[k] ? pos[k] : col4), off, 0) << (8 * k);
-            R[t] = v;
-        }
-    }
-    // sums: pixels 0 / 2 in the 16-bit lanes of *e, 1 / 3 of *o (<= 65 x 255)
-    uint32_t le = 0, lo2 = 0, re = 0, ro = 0;
-#pragma unroll
-    for (int t = 0; t < MAXN; ++t)
-        if (t < n) {
-            le += L[t] & 0x00FF00FFu;
-            lo2 += (L[t] >> 8) & 0x00FF00FFu;
-            re += R[t] & 0x00FF00FFu;
-            ro += (R[t] >> 8) & 0x00FF00FFu;
-        }
-    const uint32_t sl[4] = {le & 0xFFFFu, lo2 & 0xFFFFu, le >> 16, lo2 >> 16};
-    const uint32_t sr[4] = {re & 0xFFFFu, ro & 0xFFFFu, re >> 16, ro >> 16};
-    float m0[4], m1[4], cov[4], v0[4], v1[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        m0[k] = div_p((float)sl[k], (float)n);
-        m1[k] = div_p((float)sr[k], (float)n);
-        cov[k] = v0[k] = v1[k] = 0.f;
-    }
-#pragma unroll
-    for (int t = 0; t < MAXN; ++t)
-        if (t < n) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float x0 = (float)((L[t] >> (8 * k)) & 0xFFu) - m0[k];
-                const float x1 = (float)((R[t] >> (8 * k)) & 0xFFu) - m1[k];
-                cov[k] = fma_p(x0, x1, cov[k]);
-                v0[k] = fma_p(x0, x0, v0[k]);
-                v1[k] = fma_p(x1, x1, v1[k]);
-            }
-        }
-    float outd[4], corr[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        float c = __builtin_nanf("");
-        int dk = INVALID_I16;
-        if (inb[k]) {
-            if (a.has_minvar && (v0[k] < a.minvar || v1[k] < a.minvar))
-                c = -1.f;
-            else
-                c = div_p(cov[k], sqrt_p(v0[k] * v1[k]));
-            if (!(c < a.threshold)) dk = d[k];  // NaN passes, as in the reference
-        }
-        outd[k] = (float)dk;
-        corr[k] = c;
-    }
-    const size_t o = (size_t)row * a.cols + col4;
-    if (a.out_f32) {
-        *(float4*)((float*)a.out + o) = make_float4(outd[0], outd[1], outd[2], outd[3]);
-    } else {
-        uint2 v;
-        v.x = ((uint32_t)(int)outd[0] & 0xFFFFu) | ((uint32_t)(int)outd[1] << 16);
-        v.y = ((uint32_t)(int)outd[2] & 0xFFFFu) | ((uint32_t)(int)outd[3] << 16);
-        *(uint2*)((int16_t*)a.out + o) = v;
-    }
-    if (a.corrmap) *(float4*)((float*)a.corrmap + o) = make_float4(corr[0], corr[1], corr[2], corr[3]);
-}
-
 // ------------------------------------------------------------------- dispatch
 
 template <typename TIn, int WORDS, int MAXN>
@@ -803,36 +648,9 @@ hipError_t launch_tl(const TransformArgs& a, dim3 grid, hipStream_t st) {
     return hipGetLastError();
 }
 
-template <int WORDS, int MAXN>
-hipError_t launch_tl4(const TransformArgs& a, hipStream_t st) {
-    dim3 grid((a.cols / 4 + 255) / 256, a.rows, a.stack1 ? 2 : 1);
-    if (a.n == MAXN)
-        hipLaunchKernelGGL((transform4_kernel<WORDS, MAXN, true>), grid, dim3(256), 0, st, a);
-    else
-        hipLaunchKernelGGL((transform4_kernel<WORDS, MAXN, false>), grid, dim3(256), 0, st, a);
-    return hipGetLastError();
-}
-
-// u8 LIMITED with every dword load inside its row: 4 pixels per lane
-inline bool transform4_ok(const TransformArgs& a) {
-    const uintptr_t base = (uintptr_t)a.stack0 | (uintptr_t)(a.stack1 ? a.stack1 : a.stack0);
-    return a.cols % 4 == 0 && a.row_pitch % 4 == 0 && a.plane_pitch % 4 == 0 && base % 4 == 0;
-}
-
 template <typename TIn, int WORDS>
 hipError_t launch_transform_w(const TransformArgs& a, int mode, hipStream_t st) {
     dim3 grid((a.cols + 255) / 256, a.rows, a.stack1 ? 2 : 1);
-    if (sizeof(TIn) == 1 && mode == 0 && transform4_ok(a)) {
-        const int n = a.n;
-        if constexpr (WORDS == 1) return launch_tl4<WORDS, 9>(a, st);
-        else if constexpr (WORDS == 2) return n <= 12 ? launch_tl4<WORDS, 12>(a, st)
-                                                      : launch_tl4<WORDS, 17>(a, st);
-        else if constexpr (WORDS == 4) return n <= 24 ? launch_tl4<WORDS, 24>(a, st)
-                                                      : launch_tl4<WORDS, 33>(a, st);
-        else if (n <= 40) return launch_tl4<WORDS, 40>(a, st);
-        else if (n <= 48) return launch_tl4<WORDS, 48>(a, st);
-        else return launch_tl4<WORDS, 65>(a, st);
-    }
     if (mode == 0) {
         // descriptor width bounds n: 32 bits -> n <= 9, 64 -> 17, 128 -> 33, 256 -> 65
         const int n = a.n;
@@ -893,17 +711,6 @@ hipError_t launch_agree_m(const AgreeArgs& a, hipStream_t st) {
     const size_t sz = sizeof(TIn);
     const bool aligned = ((uintptr_t)a.stack0 % 4 == 0) && (a.row_pitch * sz) % 4 == 0 &&
                          (a.plane_pitch * sz) % 4 == 0;
-    if constexpr (sizeof(TIn) == 1 && sizeof(TPrec) == 4 && MAXN <= 40) {
-        const bool quad = aligned && a.cols % 4 == 0 && (uintptr_t)a.stack1 % 4 == 0 &&
-                          (uintptr_t)a.raw % 8 == 0 && a.raw_pitch % 4 == 0 &&
-                          (uintptr_t)a.out % (a.out_f32 ? 16 : 8) == 0 &&
-                          (uintptr_t)a.corrmap % 16 == 0;
-        if (quad) {
-            dim3 g4((a.cols / 4 + 255) / 256, a.rows);
-            hipLaunchKernelGGL((agree4_kernel<MAXN>), g4, dim3(256), 0, st, a);
-            return hipGetLastError();
-        }
-    }
     if (aligned) {
         // runtime n even for an exact bucket: with a constant n the compiler front-loads
         // the conversions and doubles the VGPRs (49 -> 100 at n = 33)

@@ -160,153 +160,5 @@ __device__ __forceinline__ void limited_descriptor(const StackReader<TIn>& rd, u
 
 }
 
-// ---- four u8 pixels per lane ---------------------------------------------------------
-//
-// The same LIMITED descriptor for the 4 consecutive u8 pixels whose samples one dword load
-// per plane brings in (4x fewer load instructions than a byte load per pixel: the
-// one-pixel-per-lane transform keeps the texture-address unit ~80 % busy, PMC in
-// profiles/pmc_stall_r03_cfg2.json). Byte k of every sample dword is pixel k; comparisons of
-// two samples (or of a sample with the packed per-pixel means) select the bytes with SDWA
-// (v_cmp_lt_u32_sdwa ... src0_sel:BYTE_k src1_sel:BYTE_k), so no byte is ever extracted,
-// and each pixel keeps its own bit accumulator: one comparison = 4 SDWA compares + 4
-// v_addc, the VALU per pixel is unchanged.
-#define BICOS_CMPB(px) \
-    "v_cmp_lt_u32_sdwa %[m" #px "], %[x], %[y] src0_sel:BYTE_" #px " src1_sel:BYTE_" #px "\n\t"
-#define BICOS_CMPW(px) "v_cmp_lt_u32_e64 %[m" #px "], %[x" #px "], %[y" #px "]\n\t"
-#define BICOS_ADD4(px) "v_addc_co_u32_e64 %[c" #px "], %[j], %[c" #px "], %[c" #px "], %[m" #px "]\n\t"
-#define BICOS_OUT4                                                                    \
-    [c0] "+v"(cur[0]), [c1] "+v"(cur[1]), [c2] "+v"(cur[2]), [c3] "+v"(cur[3]),       \
-        [m0] "=&s"(m0), [m1] "=&s"(m1), [m2] "=&s"(m2), [m3] "=&s"(m3), [j] "=&s"(j)
-
-// cur[k] = 2 cur[k] + (byte k of x < byte k of y), k = 0..3
-__device__ __forceinline__ void push4_bytes(uint32_t (&cur)[4], uint32_t x, uint32_t y) {
-    uint64_t m0, m1, m2, m3, j;
-    asm(BICOS_CMPB(0) BICOS_CMPB(1) BICOS_CMPB(2) BICOS_CMPB(3) BICOS_ADD4(0) BICOS_ADD4(1)
-            BICOS_ADD4(2) BICOS_ADD4(3)
-        : BICOS_OUT4
-        : [x] "v"(x), [y] "v"(y));
-}
-// cur[k] = 2 cur[k] + (x[k] < y[k])
-__device__ __forceinline__ void push4_words(uint32_t (&cur)[4], const uint32_t (&x)[4],
-                                            const uint32_t (&y)[4]) {
-    uint64_t m0, m1, m2, m3, j;
-    asm(BICOS_CMPW(0) BICOS_CMPW(1) BICOS_CMPW(2) BICOS_CMPW(3) BICOS_ADD4(0) BICOS_ADD4(1)
-            BICOS_ADD4(2) BICOS_ADD4(3)
-        : BICOS_OUT4
-        : [x0] "v"(x[0]), [y0] "v"(y[0]), [x1] "v"(x[1]), [y1] "v"(y[1]), [x2] "v"(x[2]),
-          [y2] "v"(y[2]), [x3] "v"(x[3]), [y3] "v"(y[3]));
-}
-#undef BICOS_CMPB
-#undef BICOS_CMPW
-#undef BICOS_ADD4
-#undef BICOS_OUT4
-
-// after the bit at static position POS: flush a full 32-bit word (MSB-first -> LSB-first)
-template <int POS, int WORDS>
-__device__ __forceinline__ void flush4(uint32_t (&cur)[4], uint32_t (&w)[4][WORDS]) {
-    if constexpr (POS % 32 == 31) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            w[k][POS / 32] = __builtin_bitreverse32(cur[k]);
-            cur[k] = 0;
-        }
-    }
-}
-
-__device__ __forceinline__ uint32_t byte_of(uint32_t v, int k) { return (v >> (8 * k)) & 0xFFu; }
-
-template <int T, int MAXN, int WORDS>
-__device__ __forceinline__ void limited_steps4(int n, uint32_t thr, const uint32_t (&v)[MAXN],
-                                               uint32_t (&ps)[2][4], uint32_t (&cur)[4],
-                                               uint32_t (&w)[4][WORDS]) {
-    if constexpr (T < MAXN - 2) {
-        if (T < n - 2) {
-            constexpr int pos = T < 2 ? 3 * T : 6 + 4 * (T - 2);
-            const uint32_t a = v[T], b = v[T + 1], c = v[T + 2];
-            push4_bytes(cur, a, b);
-            flush4<pos, WORDS>(cur, w);
-            push4_bytes(cur, a, c);
-            flush4<pos + 1, WORDS>(cur, w);
-            push4_bytes(cur, a, thr);
-            flush4<pos + 2, WORDS>(cur, w);
-            // ps[t] = a + b per pixel; ps[t-2] < ps[t] from t = 2 (descriptor_transform.hpp:52-58)
-            uint32_t cur_ps[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) cur_ps[k] = byte_of(a, k) + byte_of(b, k);
-            if constexpr (T >= 2) {
-                push4_words(cur, ps[T % 2], cur_ps);
-                flush4<pos + 3, WORDS>(cur, w);
-            }
-#pragma unroll
-            for (int k = 0; k < 4; ++k) ps[T % 2][k] = cur_ps[k];
-            limited_steps4<T + 1, MAXN, WORDS>(n, thr, v, ps, cur, w);
-        }
-    }
-}
-
-// Descriptors of the 4 u8 pixels col4 .. col4 + 3 (byte offset col4 of the row at byte
-// offset `rowoff`, plane pitch `pp` bytes; all three multiples of 4).
-template <int WORDS, int MAXN, bool EXACT>
-__device__ __forceinline__ void limited_descriptor4(const __amdgpu_buffer_rsrc_t& r, uint32_t col4,
-                                                    uint32_t rowoff, uint32_t pp, int n_rt,
-                                                    uint32_t magic, uint32_t (&w)[4][WORDS]) {
-    const int n = EXACT ? MAXN : n_rt;
-    uint32_t v[MAXN];
-#pragma unroll
-    for (int t = 0; t < MAXN; ++t)
-        if (t < n) v[t] = __builtin_amdgcn_raw_buffer_load_b32(r, col4, rowoff + (uint32_t)t * pp, 0);
-    // per-pixel sums in 16-bit lanes (pixels 0 / 2 in `se`, 1 / 3 in `so`; <= 65 x 255 fits),
-    // two ops per plane for all four pixels -- and kept apart from the pair sums the steps
-    // compare, which the compiler would otherwise keep alive from here (+64 VGPRs).
-    // ceil(sum / n) per pixel as in limited_descriptor, packed into the bytes of `thr`.
-    uint32_t se = 0, so = 0;
-#pragma unroll
-    for (int t = 0; t < MAXN; ++t) {
-        if (t < n) {
-            se += v[t] & 0x00FF00FFu;
-            so += (v[t] >> 8) & 0x00FF00FFu;
-        }
-    }
-    const uint32_t sum[4] = {se & 0xFFFFu, so & 0xFFFFu, se >> 16, so >> 16};
-    uint32_t thr = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t q = __umulhi(sum[k], magic);
-        thr |= (q + (q * (uint32_t)n != sum[k] ? 1u : 0u)) << (8 * k);
-    }
-
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int q = 0; q < WORDS; ++q) w[k][q] = 0;
-    uint32_t cur[4] = {0, 0, 0, 0};
-    uint32_t ps[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
-    limited_steps4<0, MAXN, WORDS>(n, thr, v, ps, cur, w);
-
-    // the loop's partial word and the 4 tail bits, at n-dependent positions (as in
-    // limited_descriptor; descriptor_transform.hpp:63-68)
-    const int nl = n >= 4 ? 6 + 4 * (n - 4) : 3 * (n - 2);
-    const int pw = nl >> 5, pm = nl & 31;
-    const uint32_t xv = __builtin_amdgcn_raw_buffer_load_b32(r, col4, rowoff + (uint32_t)(n - 2) * pp, 0);
-    const uint32_t yv = __builtin_amdgcn_raw_buffer_load_b32(r, col4, rowoff + (uint32_t)(n - 1) * pp, 0);
-    const uint32_t zv = n >= 4 ? __builtin_amdgcn_raw_buffer_load_b32(r, col4, rowoff + (uint32_t)(n - 4) * pp, 0) : 0u;
-    const uint32_t uv = n >= 4 ? __builtin_amdgcn_raw_buffer_load_b32(r, col4, rowoff + (uint32_t)(n - 3) * pp, 0) : 0u;
-    const int tw = nl >> 5, toff = nl & 31;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t part = pm ? __builtin_bitreverse32(cur[k] << (32 - pm)) : 0u;
-        const uint32_t x = byte_of(xv, k), y = byte_of(yv, k), th = byte_of(thr, k);
-        const uint32_t pm2 = byte_of(zv, k) + byte_of(uv, k);
-        const uint32_t tail = (uint32_t)(x < y) | ((uint32_t)(x < th) << 1) | ((uint32_t)(y < th) << 2) |
-                              ((uint32_t)(n < 4 || pm2 < x + y) << 3);
-#pragma unroll
-        for (int q = 0; q < WORDS; ++q) {
-            if (q == pw) w[k][q] |= part;
-            if (q == tw) w[k][q] |= tail << toff;
-            if (q == tw + 1 && toff > 28) w[k][q] |= tail >> (32 - toff);
-        }
-    }
-}
-
 }  // namespace
 }  // namespace bicos_hip

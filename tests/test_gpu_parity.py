@@ -70,12 +70,12 @@ def test_transform_bit_exact(gpu, oracle, n, mode, dt):
     same(out[:, : 301 * words].reshape(13, 301, words), ref)
 
 
-# u8 LIMITED stacks whose width, pitches and bases are multiples of 4 take the four-pixels-
-# per-lane transform (kernels.hip transform4_kernel): every n bucket, exact and padded, on
-# random stacks with the extreme values 0 / 255 present, and on a plane-pitch-padded view
+# u8 LIMITED transform over every n bucket, exact and padded, on random stacks with the
+# extreme values 0 / 255 present, and on a plane-pitch-padded view (a 4-pixels-per-lane
+# form of the transform was measured slower in round 3: profiles/quad_px_r03.jsonl)
 @pytest.mark.parametrize("n", [2, 3, 4, 5, 8, 9, 10, 12, 16, 17, 23, 24, 25, 32, 33, 34, 40,
                                41, 47, 48, 49, 64, 65])
-def test_transform4_bit_exact(gpu, oracle, n):
+def test_transform_limited_u8_buckets(gpu, oracle, n):
     mode = 0
     s = random_stack(n, 9, 324, np.uint8, seed=500 + n)
     s[:, 0, :8] = 0
@@ -87,7 +87,7 @@ def test_transform4_bit_exact(gpu, oracle, n):
     same(out[:, : 324 * words].reshape(9, 324, words), ref)
 
 
-def test_transform4_padded_pitches(gpu, oracle):
+def test_transform_padded_pitches(gpu, oracle):
     import torch
     n, H, W, P = 33, 11, 200, 256
     s = random_stack(n, H, W, np.uint8, seed=77)
@@ -163,13 +163,12 @@ def test_agree_bit_exact(gpu, oracle, n, dt, minvar, W):
     same(host(corr), rc)
 
 
-# u8 stacks with 4-aligned widths run agree4_kernel (4 pixels per lane): flat disparity runs
-# (one v_perm from two aligned dwords), +-1/+-2 jitter inside a lane (still one 8-byte
-# window), jumps wider than the window (the wave falls back to byte loads), matches off
-# either edge of the row, invalid pixels, NaN correlations, int16 and float outputs
+# agree over disparity patterns: flat runs, +-1/+-2 jitter, jumps, matches off either edge
+# of the row, invalid pixels, negative disparities, NaN correlations (written for a
+# 4-pixels-per-lane agree that was measured slower and dropped: profiles/quad_px_r03.jsonl)
 @pytest.mark.parametrize("n", [2, 7, 8, 16, 24, 33, 40])
 @pytest.mark.parametrize("minvar", [None, 2.0])
-def test_agree4_window_paths(gpu, oracle, n, minvar):
+def test_agree_disparity_patterns(gpu, oracle, n, minvar):
     H, W = 8, 1024
     L, R = stereo_stack(n, H, W, np.uint8, dmin=3, drange=40, seed=n + 1000)
     rng = np.random.default_rng(n)
