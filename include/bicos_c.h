@@ -226,6 +226,13 @@ int bicos_subpixel_device(const int16_t* raw, const void* stack0, const void* st
                           int rows, int cols, size_t row_pitch, size_t plane_pitch, int depth,
                           float threshold, float step, int has_minvar, float minvar_scaled,
                           float* out, float* corrmap, void* stream);
+/* agree (step <= 0) or subpixel (step > 0) in either precision: precision 1 = the CUDA
+ * build's Precision::DOUBLE NXC (corrmap is then double*); the reference kernel-bench shapes
+ * (bench/cuda.cu:99-180) time these with double precision. */
+int bicos_agree_stage_device(const int16_t* raw, const void* stack0, const void* stack1, int n,
+                             int rows, int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                             float threshold, float step, int has_minvar, float minvar_scaled,
+                             int precision, float* out, void* corrmap, void* stream);
 
 /* Build identification (arch, flags) for reports. */
 const char* bicos_build_info(void);

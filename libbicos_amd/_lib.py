@@ -58,7 +58,7 @@ EXPORTS = (
     "bicos_engine_create", "bicos_engine_default", "bicos_engine_destroy", "bicos_engine_tune", "bicos_descriptor_words", "bicos_output_type",
     "bicos_match_device", "bicos_match_device_i16", "bicos_match_host", "bicos_match_host_multi", "bicos_match_bands_device",
     "bicos_desc_pitch", "bicos_transform_device", "bicos_search_device",
-    "bicos_agree_device", "bicos_subpixel_device", "bicos_build_info",
+    "bicos_agree_device", "bicos_subpixel_device", "bicos_agree_stage_device", "bicos_build_info",
 )
 
 
@@ -141,6 +141,8 @@ def lib() -> ctypes.CDLL:
     L.bicos_agree_device.restype = I
     L.bicos_subpixel_device.argtypes = [P, P, P, I, I, I, Z, Z, I, F, F, I, F, P, P, P]
     L.bicos_subpixel_device.restype = I
+    L.bicos_agree_stage_device.argtypes = [P, P, P, I, I, I, Z, Z, I, F, F, I, F, I, P, P, P]
+    L.bicos_agree_stage_device.restype = I
     L.bicos_build_info.restype = ctypes.c_char_p
     L.bicos_build_info.argtypes = []
     _lib = L

@@ -783,7 +783,7 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
 static int agree_common(bool sub, const int16_t* raw, const void* stack0, const void* stack1,
                         int n, int rows, int cols, size_t row_pitch, size_t plane_pitch, int depth,
                         float threshold, float step, int has_minvar, float minvar_scaled,
-                        float* out, float* corrmap, void* stream) {
+                        float* out, void* corrmap, void* stream, bool dbl = false) {
     if (n < 2) return fail(BICOS_E_ARG, "need at least two images");
     if (n > 65 && sub) return fail(BICOS_E_ARG, "subpixel supports n <= 65");
     if (depth != 1 && depth != 2) return fail(BICOS_E_ARG, "bad input depth");
@@ -812,8 +812,17 @@ static int agree_common(bool sub, const int16_t* raw, const void* stack0, const 
     aa.corrmap = corrmap;
     if (int rc0 = stack_span(n, rows, cols, row_pitch, plane_pitch, depth, &aa.stack_bytes)) return rc0;
     hipStream_t st = (hipStream_t)stream;
-    return sub ? check_hip(bicos_hip::launch_subpixel(aa, depth, false, st), "subpixel launch")
-               : check_hip(bicos_hip::launch_agree(aa, depth, false, st), "agree launch");
+    return sub ? check_hip(bicos_hip::launch_subpixel(aa, depth, dbl, st), "subpixel launch")
+               : check_hip(bicos_hip::launch_agree(aa, depth, dbl, st), "agree launch");
+}
+
+int bicos_agree_stage_device(const int16_t* raw, const void* stack0, const void* stack1, int n,
+                             int rows, int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                             float threshold, float step, int has_minvar, float minvar_scaled,
+                             int precision, float* out, void* corrmap, void* stream) {
+    return agree_common(step > 0, raw, stack0, stack1, n, rows, cols, row_pitch, plane_pitch,
+                        depth, threshold, step, has_minvar, minvar_scaled, out, corrmap, stream,
+                        precision != 0);
 }
 
 int bicos_agree_device(const int16_t* raw, const void* stack0, const void* stack1, int n, int rows,

@@ -207,23 +207,26 @@ class Engine:
 
     def agree(self, raw: torch.Tensor, stack0: torch.Tensor, stack1: torch.Tensor,
               threshold: float, minvar_scaled: Optional[float] = None,
-              step: Optional[float] = None, stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+              step: Optional[float] = None, stream=None, precision: int = 0
+              ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """NXC agree (step None) or subpixel refine of an int16 search result -> (float32
+        disparity, corrmap float32 / float64 with precision=1)."""
+        if step is not None and not step > 0:
+            raise ValueError("subpixel step must be positive")
         n, rows, cols, rp, pp = _check_stack(stack0)
         out = torch.empty((rows, cols), dtype=torch.float32, device=stack0.device)
-        corr = torch.empty((rows, cols), dtype=torch.float32, device=stack0.device)
+        corr = torch.empty((rows, cols), dtype=torch.float64 if precision else torch.float32,
+                           device=stack0.device)
         hm = int(minvar_scaled is not None)
         mv = float(minvar_scaled or 0.0)
         st = _stream(stack0.device, stream)
-        if step is None:
-            rc = self._L.bicos_agree_device(raw.data_ptr(), stack0.data_ptr(), stack1.data_ptr(),
-                                            n, rows, cols, rp, pp, _depth(stack0), threshold, hm,
-                                            mv, out.data_ptr(), corr.data_ptr(), st)
-        else:
-            rc = self._L.bicos_subpixel_device(raw.data_ptr(), stack0.data_ptr(),
-                                               stack1.data_ptr(), n, rows, cols, rp, pp,
-                                               _depth(stack0), threshold, step, hm, mv,
-                                               out.data_ptr(), corr.data_ptr(), st)
-        _lib.check(rc, "bicos_agree_device")
+        rc = self._L.bicos_agree_stage_device(raw.data_ptr(), stack0.data_ptr(),
+                                              stack1.data_ptr(), n, rows, cols, rp, pp,
+                                              _depth(stack0), threshold,
+                                              -1.0 if step is None else step, hm, mv,
+                                              int(bool(precision)), out.data_ptr(),
+                                              corr.data_ptr(), st)
+        _lib.check(rc, "bicos_agree_stage_device")
         return out, corr
 
 

@@ -855,6 +855,25 @@ def test_int16_disparity_entry(gpu, n, H, W, dt, kw):
     assert (host(buf[off + H * W * 4:]) == 0xAB).all()
 
 
+@pytest.mark.parametrize("step", [None, 0.25])
+def test_agree_stage_double_equals_match(gpu, step):
+    """bicos_agree_stage_device with precision 1 (the reference kernel-bench's double NXC /
+    subpixel, tools/ref_kernel_bench.py) == the DOUBLE match on the same search result."""
+    from libbicos_amd.device import MatchConfig, descriptor_words
+    n, H, W = 10, 12, 640
+    L, R = stereo_stack(n, H, W, dmin=3, drange=30, seed=77)
+    s0, s1 = dev(L), dev(R)
+    cfg = MatchConfig(nxcorr_threshold=0.5, min_variance=1.0, subpixel_step=step, precision=1)
+    md, mc = gpu.match(s0, s1, cfg)
+    words = descriptor_words(n, 0)
+    raw = gpu.search(gpu.transform(s0, 0, words), gpu.transform(s1, 0, words), W, words, 1)
+    ad, ac = gpu.agree(raw, s0, s1, 0.5, float(np.float32(1.0) * np.float32(n)), step=step,
+                       precision=1)
+    assert ac.dtype == mc.dtype
+    same(host(ad), host(md))
+    same(host(ac), host(mc))
+
+
 def test_int16_disparity_rejects_subpixel(gpu):
     import torch
     from libbicos_amd.device import MatchConfig

@@ -148,6 +148,13 @@ for step in "$@"; do
             done ;;
         benchg2)  # the N=2 path rehearsed with gloo ranks sharing the one GPU (all line fields)
             run benchg2 600 python bench.py --gpus 2 --backend gloo --steps 5 --warmup 1 --cpu-seconds 4 ;;
+        refk) run refk 600 python tools/ref_kernel_bench.py --out gpurun_out/ref_kernel_bench.jsonl ;;
+        randsearch) run randsearch 600 python tools/random_search_bench.py --out gpurun_out/random_search.jsonl ;;
+        benchall)  # one bench line per BASELINE config + the README shape (cfg2 with host path)
+            run bench_cfg2 300 python bench.py --config cfg2 --steps 20 --warmup 3
+            for c in cfg3 cfg4 cfg5 readme cfg1; do
+                run bench_$c 300 python bench.py --config $c --steps 20 --warmup 3 --no-host-path --cpu-seconds 8
+            done ;;
         *) echo "unknown step $step" ;;
     esac
 done
