@@ -3,7 +3,7 @@ the RTX 4090 numbers it publishes (bench/baselines/cuda-rtx4090.txt). All at 330
 (bench/cuda.cu:44), random inputs as there (cv::randu over the full u8 / u16 range):
 
   transform  LIMITED with the largest stack per descriptor width (u32: n = 9, u64: 17,
-             u128: 33) and FULL (u32: 6, u64: 9, u128: 12) -- bench/cuda.cu:258-295
+             u128: 33) and FULL (u32: 6, u64: 8, u128: 12) -- bench/cuda.cu:258-295
   agree      n = 10, random disparities in [-1, 3300), threshold 0.9, min-variance 10,
              double precision -- bench/cuda.cu:99-137
   subpixel   the same, step 0.25 -- bench/cuda.cu:139-180
@@ -38,7 +38,7 @@ REF = {  # ns, bench/baselines/cuda-rtx4090.txt
     ("search", "u128"): 18821371,
 }
 LIMITED_N = {1: 9, 2: 17, 4: 33}
-FULL_N = {1: 6, 2: 9, 4: 12}
+FULL_N = {1: 6, 2: 8, 4: 12}  # max_stacksize_v FULL (impl/common.hpp:69-73)
 
 
 def timed(fn, reps):
