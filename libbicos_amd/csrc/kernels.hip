@@ -199,6 +199,31 @@ __global__ __launch_bounds__(256) void transform_limited_kernel(TransformArgs a)
     }
 }
 
+// FULL transform with the stack size N a template parameter (transform.hpp
+// full_descriptor): every bit at a static position. Used when the descriptor width is the
+// one the match picks for N (launch_transform_w); transform_kernel<..., 1> otherwise.
+template <typename TIn, int WORDS, int N>
+__global__ __launch_bounds__(256) void transform_full_kernel(TransformArgs a) {
+    const int col = blockIdx.x * 256 + threadIdx.x;
+    const int row = blockIdx.y;
+    const int which = blockIdx.z;
+    if (col >= a.cols) return;
+    const StackReader<TIn> rd(which ? a.stack1 : a.stack0, a.stack_bytes);
+    uint32_t* __restrict__ out = (which ? a.desc1 : a.desc0) + (size_t)row * a.desc_pitch + (size_t)col * WORDS;
+    uint32_t w[WORDS];
+    full_descriptor<TIn, WORDS, N>(rd, (uint32_t)col, (uint32_t)row * (uint32_t)a.row_pitch,
+                                   (uint32_t)a.plane_pitch, a.magic, w);
+    if (WORDS % 4 == 0) {
+#pragma unroll
+        for (int k = 0; k < WORDS; k += 4)
+            *(uint4*)(out + k) = make_uint4(w[k], w[k + 1], w[k + 2], w[k + 3]);
+    } else if (WORDS == 2) {
+        *(uint2*)out = make_uint2(w[0], w[1 % WORDS]);
+    } else {
+        out[0] = w[0];
+    }
+}
+
 // --------------------------------------------------------------------- search
 
 // Hamming cost of one (col0, col1) pair.
@@ -663,6 +688,21 @@ hipError_t launch_transform_w(const TransformArgs& a, int mode, hipStream_t st) 
         else if (n <= 48) return launch_tl<TIn, WORDS, 48>(a, grid, st);
         else return launch_tl<TIn, WORDS, 65>(a, grid, st);
     }
+    // FULL: n^2 - 2n + 3 bits; the static kernel for the width the match uses for n
+#define BICOS_FULL_N(N)                                                                   \
+    case N:                                                                               \
+        if constexpr (WORDS == (N * N - 2 * N + 3 <= 32 ? 1 : N * N - 2 * N + 3 <= 64 ? 2  \
+                                : N * N - 2 * N + 3 <= 128 ? 4 : 8)) {                     \
+            hipLaunchKernelGGL((transform_full_kernel<TIn, WORDS, N>), grid, dim3(256), 0, st, a); \
+            return hipGetLastError();                                                     \
+        }                                                                                 \
+        break;
+    switch (a.n) {
+        BICOS_FULL_N(2) BICOS_FULL_N(3) BICOS_FULL_N(4) BICOS_FULL_N(5) BICOS_FULL_N(6)
+        BICOS_FULL_N(7) BICOS_FULL_N(8) BICOS_FULL_N(9) BICOS_FULL_N(10) BICOS_FULL_N(11)
+        BICOS_FULL_N(12) BICOS_FULL_N(13) BICOS_FULL_N(14) BICOS_FULL_N(15) BICOS_FULL_N(16)
+    }
+#undef BICOS_FULL_N
     hipLaunchKernelGGL((transform_kernel<TIn, WORDS, 1>), grid, dim3(256), 0, st, a);
     return hipGetLastError();
 }

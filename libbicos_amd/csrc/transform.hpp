@@ -160,5 +160,88 @@ __device__ __forceinline__ void limited_descriptor(const StackReader<TIn>& rd, u
 
 }
 
+// ---- FULL transform with a compile-time stack size ---------------------------------
+//
+// descriptor_transform.hpp:75-123: per t < n-2 the bits a<b, a<c, a<av; then the last pair's
+// a<b, a<av, b<av; then every pair sum against every pair sum that is not itself or a
+// neighbour, ps[t] < ps[i] for t, i < n-1 in (t, i) order -- n^2 - 2n + 3 bits. With n a
+// template parameter every bit position is static, so the bits go through the same
+// compare -> SGPR mask -> v_addc groups as the LIMITED transform (emit_bits), four at a
+// time, with static 32-bit flushes and no per-bit branches.
+template <int N>
+struct FullOrder {
+    static constexpr int M = N >= 3 ? (N - 3) * (N - 2) : 0;  // pair-sum comparisons
+    int t[M > 0 ? M : 1], i[M > 0 ? M : 1];
+    constexpr FullOrder() : t(), i() {
+        int k = 0;
+        for (int a = 0; a < N - 1; ++a)
+            for (int b = 0; b < N - 1; ++b) {
+                if (b == a || b == a - 1 || b == a + 1) continue;
+                t[k] = a;
+                i[k] = b;
+                ++k;
+            }
+    }
+};
+
+// groups of 4 pair-sum comparisons from comparison 4G on, at bit BASE + 4G
+template <int N, int WORDS, int BASE, int G>
+__device__ __forceinline__ void full_pair_groups(uint32_t& cur, uint32_t (&w)[WORDS],
+                                                 const uint32_t (&ps)[N > 1 ? N - 1 : 1]) {
+    constexpr FullOrder<N> ord{};
+    if constexpr (4 * G < FullOrder<N>::M) {
+        constexpr int K = FullOrder<N>::M - 4 * G < 4 ? FullOrder<N>::M - 4 * G : 4;
+        uint32_t x[4] = {0, 0, 0, 0}, y[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int q = 0; q < K; ++q) {
+            x[q] = ps[ord.t[4 * G + q]];
+            y[q] = ps[ord.i[4 * G + q]];
+        }
+        emit_bits<BASE + 4 * G, K, WORDS>(cur, w, x, y);
+        full_pair_groups<N, WORDS, BASE, G + 1>(cur, w, ps);
+    }
+}
+
+template <int T, int N, int WORDS>
+__device__ __forceinline__ void full_steps(uint32_t thr, const uint32_t (&v)[N], uint32_t& cur,
+                                           uint32_t (&w)[WORDS]) {
+    if constexpr (T < N - 2) {
+        const uint32_t x[4] = {v[T], v[T], v[T], 0}, y[4] = {v[T + 1], v[T + 2], thr, 0};
+        emit_bits<3 * T, 3, WORDS>(cur, w, x, y);
+        full_steps<T + 1, N, WORDS>(thr, v, cur, w);
+    }
+}
+
+template <typename TIn, int WORDS, int N>
+__device__ __forceinline__ void full_descriptor(const StackReader<TIn>& rd, uint32_t col,
+                                                uint32_t rowoff, uint32_t pp, uint32_t magic,
+                                                uint32_t (&w)[WORDS]) {
+    static_assert(N >= 2 && N * N - 2 * N + 3 <= 32 * WORDS, "descriptor too narrow");
+    uint32_t v[N];
+    uint32_t sum = 0;
+#pragma unroll
+    for (int t = 0; t < N; ++t) {
+        v[t] = rd(col, rowoff + (uint32_t)t * pp);
+        sum += v[t];
+    }
+    // a < av  <=>  a < ceil(sum / n) (see limited_descriptor)
+    const uint32_t q = __umulhi(sum, magic);
+    const uint32_t thr = q + (q * (uint32_t)N != sum ? 1u : 0u);
+    uint32_t ps[N > 1 ? N - 1 : 1];
+#pragma unroll
+    for (int t = 0; t + 1 < N; ++t) ps[t] = v[t] + v[t + 1];
+#pragma unroll
+    for (int k = 0; k < WORDS; ++k) w[k] = 0;
+    uint32_t cur = 0;
+    full_steps<0, N, WORDS>(thr, v, cur, w);
+    {
+        const uint32_t x[4] = {v[N - 2], v[N - 2], v[N - 1], 0}, y[4] = {v[N - 1], thr, thr, 0};
+        emit_bits<3 * (N - 2), 3, WORDS>(cur, w, x, y);
+    }
+    full_pair_groups<N, WORDS, 3 * (N - 2) + 3, 0>(cur, w, ps);
+    constexpr int B = N * N - 2 * N + 3;
+    if constexpr (B % 32 != 0) w[B / 32] = __builtin_bitreverse32(cur << (32 - B % 32));
+}
+
 }  // namespace
 }  // namespace bicos_hip

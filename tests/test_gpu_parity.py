@@ -70,6 +70,26 @@ def test_transform_bit_exact(gpu, oracle, n, mode, dt):
     same(out[:, : 301 * words].reshape(13, 301, words), ref)
 
 
+# FULL transform, every n it supports (2..16: each its own static kernel), u8 and u16,
+# extreme values present; and a wider descriptor than the match would pick (the generic
+# kernel)
+@pytest.mark.parametrize("n", list(range(2, 17)))
+@pytest.mark.parametrize("dt", [np.uint8, np.uint16])
+def test_transform_full_every_n(gpu, oracle, n, dt):
+    s = random_stack(n, 6, 257, dt, seed=900 + n)
+    s[:, 0, :5] = 0
+    s[:, 1, :5] = np.iinfo(dt).max
+    words = oracle.desc_words(n, 1)
+    ref = oracle.transform(s, 1, words)
+    out = host(gpu.transform(dev(s), 1, words)).view(np.uint32)
+    same(out[:, : 257 * words].reshape(6, 257, words), ref)
+    if words < 8:
+        wide = 2 * words
+        ref2 = oracle.transform(s, 1, wide)
+        out2 = host(gpu.transform(dev(s), 1, wide)).view(np.uint32)
+        same(out2[:, : 257 * wide].reshape(6, 257, wide), ref2)
+
+
 # u8 LIMITED transform over every n bucket, exact and padded, on random stacks with the
 # extreme values 0 / 255 present, and on a plane-pitch-padded view (a 4-pixels-per-lane
 # form of the transform was measured slower in round 3: profiles/quad_px_r03.jsonl)
