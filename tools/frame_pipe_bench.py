@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--streams", default="1,2", help="stream counts S to compare")
+    ap.add_argument("--tunes", default="0:0:0:0",
+                    help="search geometries to compare, each variant:T:waves:LDS-KiB "
+                         "(bicos_engine_tune; 0:0:0:0 = the default)")
     args = ap.parse_args()
     Ss = [int(v) for v in args.streams.split(",")]
     SM = max(Ss + [2])
@@ -38,7 +41,10 @@ def main():
     mcfg = device.MatchConfig(**C["cfg"])
     engines = [device.Engine(0) for _ in range(SM)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(SM - 1)]
-    for N in [int(v) for v in args.ns.split(",")]:
+    tunes = [tuple(int(x) for x in t.split(":")) for t in args.tunes.split(",")]
+    for N, tune in [(N, t) for N in [int(v) for v in args.ns.split(",")] for t in tunes]:
+        for e_ in engines:
+            e_.tune(*tune)
         b, e = band_rows(H, N, 0)
         rows = e - b
         L, R = stereo_stack(n, H, W, np.uint8, row_begin=b, row_end=e)
@@ -67,6 +73,7 @@ def main():
                 res[S].append((time.perf_counter() - t0) / args.reps * 1e3)
         for S in Ss:
             print(json.dumps({"config": args.config, "N": N, "band_rows": rows, "streams": S,
+                              "tune": ":".join(map(str, tune)),
                               "ms_per_frame": round(statistics.median(res[S]), 4),
                               "ms_min": round(min(res[S]), 4)}), flush=True)
 

@@ -148,6 +148,8 @@ for step in "$@"; do
             done ;;
         benchg2)  # the N=2 path rehearsed with gloo ranks sharing the one GPU (all line fields)
             run benchg2 600 python bench.py --gpus 2 --backend gloo --steps 5 --warmup 1 --cpu-seconds 4 ;;
+        tunepipe)  # search geometries that leave wave slots for the other frames' HBM stages
+            run tunepipe 600 python tools/frame_pipe_bench.py --ns 1 --streams 1,2,3 --rounds 2 --reps 40 --tunes ${TUNES:-0:0:0:0,64:4:4:48,64:4:4:40,64:4:6:64,64:2:8:64,64:4:8:64} ;;
         refk) run refk 600 python tools/ref_kernel_bench.py --out gpurun_out/ref_kernel_bench.jsonl ;;
         randsearch) run randsearch 600 python tools/random_search_bench.py --out gpurun_out/random_search.jsonl ;;
         benchall)  # one bench line per BASELINE config + the README shape (cfg2 with host path)
