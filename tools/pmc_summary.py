@@ -87,10 +87,13 @@ def main():
             if tot:
                 d["l2_hit_rate"] = round(d["TCC_HIT_sum"] / tot, 4)
         if d.get("GRBM_GUI_ACTIVE"):
+            # GRBM_GUI_ACTIVE is summed over the 8 XCDs (8 x the kernel's cycles: the search's
+            # value / 8 matches its duration at the clock it holds); TA_TA_BUSY / TD_TD_BUSY
+            # are summed over their instances, one per CU
             for c in ("TA_TA_BUSY_sum", "TD_TD_BUSY_sum"):
-                if c in d:  # summed over the TA/TD instances: one per CU
+                if c in d:
                     d[c.replace("_sum", "").lower() + "_frac_per_cu"] = round(
-                        d[c] / d["GRBM_GUI_ACTIVE"] / 256, 4)
+                        d[c] / (d["GRBM_GUI_ACTIVE"] / 8) / 256, 4)
         out["kernels"][key] = d
     os.makedirs(os.path.dirname(dst) or ".", exist_ok=True)
     json.dump(out, open(dst, "w"), indent=1)
