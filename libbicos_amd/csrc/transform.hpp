@@ -1,7 +1,7 @@
-// transform.hpp -- the LIMITED descriptor of one pixel (reference
-// include/impl/cpu/descriptor_transform.hpp:31-73), shared by transform_limited_kernel
-// (kernels.hip) and the fused transform -> search of the matrix-core search (search_mx.hip,
-// descriptors built straight into LDS / registers from the stacks).
+// transform.hpp -- the descriptor of one pixel, LIMITED (reference
+// include/impl/cpu/descriptor_transform.hpp:31-73, limited_descriptor) and FULL with the
+// stack size static (descriptor_transform.hpp:75-123, full_descriptor), used by
+// transform_limited_kernel / transform_full_kernel in kernels.hip.
 #pragma once
 
 #include "stack.hpp"

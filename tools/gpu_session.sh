@@ -128,6 +128,16 @@ for step in "$@"; do
                 run abpipe_alt$k 300 python tools/frame_pipe_bench.py --ns 1,8 --streams 1,3 --rounds 2
             done
             cp build/cur.so libbicos_amd/libbicos_amd.so ;;
+        abtf)  # transform stage alone (reference kernel-bench shapes) + one config's frame: current lib vs build/alt.so
+            cp libbicos_amd/libbicos_amd.so build/cur.so
+            for k in 1 2; do
+                for l in cur alt; do
+                    cp build/$l.so libbicos_amd/libbicos_amd.so
+                    run abtf_${l}$k 300 python tools/ref_kernel_bench.py --stages transform --reps 40
+                    run abtfb_${l}$k 300 python bench.py --config ${SC:-readme} --steps 10 --warmup 2 --no-cpu-baseline --no-host-path
+                done
+            done
+            cp build/cur.so libbicos_amd/libbicos_amd.so ;;
         pmchead)  # HBM bytes per in-frame dispatch at HEAD: FETCH_SIZE and WRITE_SIZE passes per
                   # config / band (PMCSETS="cfg2:1 cfg2:8 ..."), summarised by tools/pmc_summary.py
             mkdir -p gpurun_out/pmc

@@ -67,7 +67,10 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=20)
     ap.add_argument("--out", default="")
+    ap.add_argument("--stages", default="transform,agree,search",
+                    help="comma list of transform / agree (agree + subpixel) / search")
     args = ap.parse_args()
+    stages = set(args.stages.split(","))
     eng = device.Engine(0)
     g = torch.Generator(device="cuda")
     g.manual_seed(0x600DF00D)
@@ -82,7 +85,7 @@ def main():
         print(json.dumps(d), flush=True)
 
     for dt in ("u8", "u16"):
-        for mode, table in ((0, LIMITED_N), (1, FULL_N)):
+        for mode, table in ((0, LIMITED_N), (1, FULL_N)) if "transform" in stages else ():
             for words, n in table.items():
                 s = rand_stack(n, dt, g)
                 out = eng.transform(s, mode, words)
@@ -93,6 +96,8 @@ def main():
                       "GBps": round(px * (n * (1 if dt == "u8" else 2) + 4 * words) / ms / 1e6, 1),
                       "key": ("transform", dt, mode, words)})
                 del s, out
+        if "agree" not in stages:
+            continue
         n = 10
         s0, s1 = rand_stack(n, dt, g), rand_stack(n, dt, g)
         raw = torch.randint(-1, W, (H, W), dtype=torch.int16, device="cuda", generator=g)
@@ -104,14 +109,15 @@ def main():
                       "step": step, "threshold": 0.9, "minvar_scaled": 10.0, "ms": round(ms, 4),
                       "key": (stage, dt) if prec else None})
         del s0, s1, raw
-    words = 4
-    pitch = eng._L.bicos_desc_pitch(W, words)
-    d0 = torch.randint(-2 ** 31, 2 ** 31 - 1, (H, pitch), dtype=torch.int32, device="cuda", generator=g)
-    d1 = torch.randint(-2 ** 31, 2 ** 31 - 1, (H, pitch), dtype=torch.int32, device="cuda", generator=g)
-    out = eng.search(d0, d1, W, words, 1)
-    ms = timed(lambda: eng.search(d0, d1, W, words, 1, out=out), max(3, args.reps // 4))
-    emit({"stage": "search", "input": "random u128 descriptors", "flags": "NODUPES",
-          "ms": round(ms, 4), "key": ("search", "u128")})
+    if "search" in stages:
+        words = 4
+        pitch = eng._L.bicos_desc_pitch(W, words)
+        d0 = torch.randint(-2 ** 31, 2 ** 31 - 1, (H, pitch), dtype=torch.int32, device="cuda", generator=g)
+        d1 = torch.randint(-2 ** 31, 2 ** 31 - 1, (H, pitch), dtype=torch.int32, device="cuda", generator=g)
+        out = eng.search(d0, d1, W, words, 1)
+        ms = timed(lambda: eng.search(d0, d1, W, words, 1, out=out), max(3, args.reps // 4))
+        emit({"stage": "search", "input": "random u128 descriptors", "flags": "NODUPES",
+              "ms": round(ms, 4), "key": ("search", "u128")})
     if args.out:
         with open(args.out, "a") as f:
             for d in lines:
