@@ -110,7 +110,9 @@ void bicos_engine_destroy(bicos_engine* e);
  *   waves          waves per workgroup (1..8)
  *   split          waves that share one col0 group and split its col1 scan (1|2|4|8)
  * Matrix-core search (search_mx.hip, the default): variant 64 (automatic keys), 65 (one FP4
- * product per pair + xor keys; rows <= 16384), 66 (two products: first / last minimum);
+ * product per pair + xor keys; rows <= 16384), 66 (two products: first / last minimum), 67
+ * (xor keys for first-minimum searches too, instead of the float keys that carry the column
+ * in a free K half);
  * col0_per_lane = 32-column tiles per wave (2|4|8; 8 falls back to 4 where the registers do
  * not fit), waves 1..8, split = LDS stage KiB (0 = 64).
  * Results are identical for every setting; only speed changes. */

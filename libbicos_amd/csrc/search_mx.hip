@@ -257,7 +257,11 @@ void search_mx_kernel(SearchArgs a) {
 
     // PAIRS (KEYS 2): the running first minima of tiles 2p / 2p+1 share register mp[p]
     // (lanes 0-31 / 32-63: the halves that write those tiles), see block()
+#if defined(BICOS_MX_DIAG) && BICOS_MX_DIAG <= 2
+    constexpr bool PAIRS = false;  // diagnostic floors reduce per tile (m1[] must stay live)
+#else
     constexpr bool PAIRS = FREE && T % 2 == 0;
+#endif
     // one pair per wave: the block loop is software-pipelined (see the FREE chunk loop)
     constexpr bool PIPE = PAIRS && T == 2;
     // XK full blocks: the next block's A fragments are read while this one is reduced.
@@ -355,8 +359,16 @@ void search_mx_kernel(SearchArgs a) {
         const auto sw = __builtin_amdgcn_permlane32_swap(x, y, false, false);
         const uint32_t comb = min((uint32_t)sw[0], (uint32_t)sw[1]);
         const uint32_t ms = mp[p] - (uint32_t)(B - bprev);
+#if defined(BICOS_MX_DIAG) && BICOS_MX_DIAG == 4  // timing only: the last-minimum path never runs
+        const bool reach = comb <= (ms | XK_COL) && comb == 0u;
+#else
         const bool reach = comb <= (ms | XK_COL);  // cost <= running minimum cost
+#endif
         mp[p] = min(ms, comb);
+#if defined(BICOS_MX_DIAG) && BICOS_MX_DIAG == 5  // timing only: no last-minimum branch at all
+        if (reach) m2[2 * p] ^= 0u;
+        return;
+#endif
         const uint64_t bal = __builtin_amdgcn_ballot_w64(reach);
         // (halves as opaque SGPRs: left alone the compiler tests the upper one with a 64-bit
         // VALU compare)
@@ -426,7 +438,7 @@ void search_mx_kernel(SearchArgs a) {
             v4i af[KS], an[KS];
 #pragma unroll
             for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + 32 * b + j];
-#if !defined(BICOS_MX_DIAG)
+#if !defined(BICOS_MX_DIAG) || BICOS_MX_DIAG >= 3
             if constexpr (FREE && PAIRS) {
 #pragma unroll
                 for (int p = 0; p < T / 2; ++p) {
@@ -503,7 +515,7 @@ void search_mx_kernel(SearchArgs a) {
             if (partial) partial_block(cc);
             // full blocks downwards from the one holding the wave's highest col0 (clamped)
             const int sb = max(0, min(nfull - 1, (c0_wave + 32 * T - 1 - base) / 32));
-#if !defined(BICOS_MX_DIAG)
+#if !defined(BICOS_MX_DIAG) || BICOS_MX_DIAG >= 3
             if constexpr (PIPE) {
                 // software pipeline over the blocks (one tile pair per wave): the products of
                 // block i+1 are issued before block i is reduced, so the wave's MFMAs stay in
@@ -704,10 +716,8 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     // step to drop (129..192 used bits)
     g.ksteps = words >= 2 ? words / 2 : 1;
     if (words == 8 && bits > 0 && bits <= 192) g.ksteps = 3;
-    // BICOS_MX_FK=0: XK keys for the first-minimum searches too (A/B; read per call)
-    const char* fk_v = std::getenv("BICOS_MX_FK");
-    const bool fk_env = !(fk_v && fk_v[0] == '0');
-    g.fk = fk_env && g.keys == 1 && bits > 0 && bits <= 64 * g.ksteps - 32 && cols <= FK_MAX_COLS;
+    // keys 3 (engine tuned to variant 67): XK keys for the first-minimum searches too (A/B)
+    g.fk = keys != 3 && g.keys == 1 && bits > 0 && bits <= 64 * g.ksteps - 32 && cols <= FK_MAX_COLS;
     const int wl = 2 * g.ksteps;
     // LDS chunk of expanded right descriptors (16 B per word per col1), multiple of 32
     int chunk = lds_bytes / (wl * 16);

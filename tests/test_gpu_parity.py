@@ -5,6 +5,7 @@ Bar (north star): integer disparities bit-exact; nxcorr / subpixel floats within
 demand exact equality (the tolerance is only used for Precision::DOUBLE, which
 has no CPU oracle: |corr - float64 numpy| <= 1e-12).
 """
+import contextlib
 import numpy as np
 import pytest
 
@@ -480,6 +481,16 @@ def test_valu_consistency_edges(gpu, oracle, n, H, W, maxval, no_dupes):
         same(d, rd)
 
 
+@contextlib.contextmanager
+def xk_keys(eng):
+    """The matrix-core search with XK keys for first-minimum searches too (no FK keys)."""
+    eng.tune(67)
+    try:
+        yield
+    finally:
+        eng.tune(0)
+
+
 @pytest.mark.parametrize("n,H,W,dt,kw", [
     (40, 6, 2048, np.uint8, dict(variant=1, max_lr_diff=1)),   # widest FK row (|col1 - B| < 2048)
     (40, 3, 2049, np.uint8, dict(variant=1, max_lr_diff=1)),   # one column more: XK keys
@@ -487,13 +498,12 @@ def test_valu_consistency_edges(gpu, oracle, n, H, W, maxval, no_dupes):
     (8, 5, 700, np.uint16, dict(variant=1, max_lr_diff=0)),    # 32-bit descriptors
     (33, 4, 640, np.uint8, dict(variant=1, max_lr_diff=1)),    # 125 bits: no free half, XK
 ])
-def test_fk_keys_equal_xk_keys(gpu, oracle, n, H, W, dt, kw, monkeypatch):
+def test_fk_keys_equal_xk_keys(gpu, oracle, n, H, W, dt, kw):
     """KEYS 3 (float keys, the column carried in the free K half with an E8M0 scale of
-    2^-12, C = 0) against the XK keys (BICOS_MX_FK=0) and the oracle."""
+    2^-12, C = 0) against the XK keys (engine tuned to variant 67) and the oracle."""
     L, R = stereo_stack(n, H, W, dt, dmin=2, drange=40, seed=n * 13 + W)
-    monkeypatch.setenv("BICOS_MX_FK", "0")
-    d_x, c_x = gpu_match(gpu, L, R, **kw)
-    monkeypatch.setenv("BICOS_MX_FK", "1")
+    with xk_keys(gpu):
+        d_x, c_x = gpu_match(gpu, L, R, **kw)
     d_f, c_f = gpu_match(gpu, L, R, **kw)
     same(d_f, d_x)
     if c_x is not None:
@@ -503,7 +513,7 @@ def test_fk_keys_equal_xk_keys(gpu, oracle, n, H, W, dt, kw, monkeypatch):
 
 
 @pytest.mark.parametrize("words,bits,W", [(8, 150, 2048), (8, 160, 1000), (4, 90, 777), (1, 32, 301)])
-def test_fk_search_ties(gpu, words, bits, W, monkeypatch):
+def test_fk_search_ties(gpu, words, bits, W):
     """First-minimum search (flags 0) on low-entropy descriptors (few set bits: many equal
     costs, so the lowest-col1 tie rule decides most pixels): FK keys == XK keys == numpy."""
     import torch
@@ -525,9 +535,8 @@ def test_fk_search_ties(gpu, words, bits, W, monkeypatch):
     d0, d1 = desc(), desc()
     t0 = torch.from_numpy(d0.view(np.int32)).cuda()
     t1 = torch.from_numpy(d1.view(np.int32)).cuda()
-    monkeypatch.setenv("BICOS_MX_FK", "0")
-    ox = host(gpu.search(t0, t1, W, words, flags=0, bits=bits))
-    monkeypatch.setenv("BICOS_MX_FK", "1")
+    with xk_keys(gpu):
+        ox = host(gpu.search(t0, t1, W, words, flags=0, bits=bits))
     of = host(gpu.search(t0, t1, W, words, flags=0, bits=bits))
     same(of, ox)
     # numpy: popcount Hamming, lowest col1 among the minima, disparity = col0 - col1
