@@ -138,6 +138,17 @@ for step in "$@"; do
                 done
             done
             cp build/cur.so libbicos_amd/libbicos_amd.so ;;
+        abbench)  # whole bench lines over several builds (LIBS="a b ..." = build/<x>.so, SCS configs), interleaved twice
+            cp libbicos_amd/libbicos_amd.so build/cur.so
+            for k in 1 2; do
+                for c in ${SCS:-cfg2}; do
+                    for l in ${LIBS}; do
+                        cp build/$l.so libbicos_amd/libbicos_amd.so
+                        run abb_${c}_${l}_$k 300 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline --no-host-path
+                    done
+                done
+            done
+            cp build/cur.so libbicos_amd/libbicos_amd.so ;;
         pmchead)  # HBM bytes per in-frame dispatch at HEAD: FETCH_SIZE and WRITE_SIZE passes per
                   # config / band (PMCSETS="cfg2:1 cfg2:8 ..."), summarised by tools/pmc_summary.py
             mkdir -p gpurun_out/pmc
