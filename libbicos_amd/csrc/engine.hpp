@@ -88,11 +88,6 @@ int reserve(void*& buf, size_t& have, size_t bytes, int device, hipStream_t st, 
 int descriptor_words(int n, int mode);
 
 bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, int words);
-// Consistency runs the fused search unless BICOS_CONSISTENCY=twopass
-bool fused_consistency();
-// geometry of the fused Consistency search (row stage + per-column keys in LDS)
-bicos_hip::SearchGeometry geometry_lr(const bicos_engine* e, int rows, int cols, int words,
-                                      bool nodupes);
 
 // Full match on device buffers (validated arguments). corr may be null. disp_i16: the
 // disparity map is int16 even with the NXC stage (no subpixel; bicos_match_device_i16).

@@ -1,6 +1,5 @@
 // nxc.hpp -- device helpers of the NXC agree (reference include/impl/cpu/agree.hpp:28-93)
-// shared by the standalone agree kernels (kernels.hip) and the search epilogues that fuse
-// the agree (search16_kernel<..., FUSE>, search_mx_kernel<..., FUSE>).
+// shared by the agree kernels (kernels.hip) and the subpixel refine (subpixel.hpp).
 //
 // Numerics: every float op is an explicit IEEE round-to-nearest op (the sources are compiled
 // with -ffp-contract=off), fmaf exactly where the reference calls std::fmaf, correctly
