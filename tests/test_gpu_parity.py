@@ -108,15 +108,27 @@ def test_transform_limited_u8_buckets(gpu, oracle, n):
     same(out[:, : 324 * words].reshape(9, 324, words), ref)
 
 
-def test_transform_padded_pitches(gpu, oracle):
+@pytest.mark.parametrize("n,mode,dt,W,P", [
+    (33, 0, np.uint8, 200, 256),    # dword-aligned rows
+    (33, 0, np.uint8, 201, 257),    # odd byte pitch
+    (17, 0, np.uint16, 301, 302),   # u16, 604-byte rows
+    (17, 0, np.uint16, 301, 303),   # u16, 606-byte rows
+    (12, 1, np.uint8, 259, 260),    # FULL (static-n kernel)
+    (12, 1, np.uint8, 259, 261),
+    (9, 0, np.uint8, 5, 8),         # one partial tile
+])
+def test_transform_padded_pitches(gpu, oracle, n, mode, dt, W, P):
+    """Padded row pitches / plane strides (aligned and odd), u8 / u16, LIMITED / FULL,
+    against the oracle."""
     import torch
-    n, H, W, P = 33, 11, 200, 256
-    s = random_stack(n, H, W, np.uint8, seed=77)
-    buf = torch.zeros((n, H + 3, P), dtype=torch.uint8, device="cuda")
+    H = 11
+    s = random_stack(n, H, W, dt, seed=77 + W)
+    tdt = torch.uint8 if dt == np.uint8 else torch.int16
+    buf = torch.zeros((n, H + 3, P), dtype=tdt, device="cuda")
     buf[:, :H, :W] = dev(s)
-    words = oracle.desc_words(n, 0)
-    out = host(gpu.transform(buf[:, :H, :W], 0, words)).view(np.uint32)
-    same(out[:, : W * words].reshape(H, W, words), oracle.transform(s, 0, words))
+    words = oracle.desc_words(n, mode)
+    out = host(gpu.transform(buf[:, :H, :W], mode, words)).view(np.uint32)
+    same(out[:, : W * words].reshape(H, W, words), oracle.transform(s, mode, words))
 
 
 # -------------------------------------------------------------------- search
