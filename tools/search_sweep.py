@@ -30,6 +30,7 @@ def main():
     ap.add_argument("--rows", type=int, default=0, help="row band size (0 = full frame)")
     ap.add_argument("--variants", default="0:0:0,16:2:8,16:4:8,16:2:4,16:4:4")
     ap.add_argument("--all-bits", action="store_true", help="no used-bits hint (all K-steps)")
+    ap.add_argument("--random", action="store_true", help="random descriptors (u128 kernel-bench input)")
     args = ap.parse_args()
     C = bench.CONFIGS[args.config]
     n, H, W = C["n"], C["H"], C["W"]
@@ -45,6 +46,16 @@ def main():
     bits = 0 if args.all_bits else device.used_bits(n, cfg.mode)
     variants = [tuple(int(x) for x in v.split(":")) for v in args.variants.split(",")]
     variants = [v + (0,) * (4 - len(v)) for v in variants]
+    if args.random:
+        g = torch.Generator(device="cuda").manual_seed(1)
+        for d in (d0, d1):
+            d.copy_(torch.randint(-2**31, 2**31 - 1, d.shape, dtype=torch.int32, device="cuda", generator=g))
+            if bits:  # only the bits the transform would set (the FK keys need the rest 0)
+                v = d[:, :W * words].view(rows, W, words)
+                for q in range(words):
+                    keep = 0 if 32 * q >= bits else min(32, bits - 32 * q)
+                    m = (1 << keep) - 1
+                    v[:, :, q] &= (m - (1 << 32) if m >= 1 << 31 else m)
     times = {v: [] for v in variants}
     ref = None
     st = torch.cuda.current_stream()
@@ -68,7 +79,7 @@ def main():
     for v in variants:
         med, mn = statistics.median(times[v]), min(times[v])
         print(json.dumps({"config": args.config, "rows": rows, "variant": v[0], "col0_per_lane": v[1],
-                          "waves": v[2], "split": v[3], "ms_median": round(med, 4), "ms_min": round(mn, 4),
+                          "waves": v[2], "split": v[3], "random": args.random, "ms_median": round(med, 4), "ms_min": round(mn, 4),
                           "Tops": round(ops / (med * 1e-3) / 1e12, 2)}))
 
 
