@@ -289,6 +289,12 @@ def main():
                          "timed run, NB more steps land over a sentinel and rank 0 checks every "
                          "gather slot's whole frame against the oracle's sha256 in "
                          "tests/golden/frames.json, or a one-GPU match of the whole frame)")
+    ap.add_argument("--gather-rehearsal", action="store_true",
+                    help="one rank, and still the whole N>1 gather path on a 1-rank process group "
+                         "(--backend nccl: RCCL init, the packed band buffer gathered from the "
+                         "match's streams, the int16 landing, the gather timing and the frame "
+                         "verification) -- rehearses the RCCL branch on a one-GPU box (not a "
+                         "measurement)")
     ap.add_argument("--band-of", type=int, default=1,
                     help="one process, band 0 of an N-way row split (no gather): the band a "
                          "rank of an N-GPU run computes, for profiling at band sizes")
@@ -337,11 +343,22 @@ def main():
     local_dev = local % ndev
     torch.cuda.set_device(local_dev)
     dev = torch.device("cuda", local_dev)
-    if world > 1:
+    if args.gather_rehearsal and world != 1:
+        raise SystemExit("--gather-rehearsal runs one rank")
+    # a process group whenever the gather path runs (N > 1, or the 1-rank rehearsal)
+    dist_on = world > 1 or args.gather_rehearsal
+    if dist_on:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            if "MASTER_PORT" not in os.environ:
+                import socket
+                with socket.socket() as so:
+                    so.bind(("127.0.0.1", 0))
+                    os.environ["MASTER_PORT"] = str(so.getsockname()[1])
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
         else:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", rank=rank, world_size=world)
 
     C = CONFIGS[args.config]
     n, H, W = C["n"], C["H"], C["W"]
@@ -374,7 +391,7 @@ def main():
              for _ in range(F)]
     out, corr = outs[0], corrs[0]
 
-    gather = world > 1 and args.scaling == "strong"
+    gather = dist_on and args.scaling == "strong"
     nccl = args.backend == "nccl"
     # integer disparities (NXC without subpixel): the band ships its disparity as int16 --
     # (float) of it IS the float map -- and rank 0 converts the gathered frame back to float32
@@ -529,7 +546,10 @@ def main():
         hp = host_path(C, mcfg, reps=5)
 
     if rank == 0:
-        if gather:
+        if gather and args.gather_rehearsal:
+            par = ("rehearsal: the row-band gather path on a 1-rank %s process group (self-"
+                   "gather; not a measurement)" % ("RCCL" if nccl else "gloo"))
+        elif gather:
             par = ("row-bands x%d + RCCL gather over xGMI" % world if nccl else
                    "gloo rehearsal: row-bands x%d + gloo gather, ranks sharing %d GPU(s) "
                    "(not a measurement)" % (world, ndev))
@@ -559,7 +579,7 @@ def main():
                 "n_images": n, "rows": H, "cols": W, "descriptor_bits": 32 * words,
                 "rows_per_rank": rows,
                 "parallelism": par,
-                "backend": args.backend if world > 1 else None,
+                "backend": args.backend if dist_on else None,
                 "match_config": C["cfg"],
             },
             "roofline": roof,
@@ -574,7 +594,7 @@ def main():
                                         ours_ms_one_at_a_time=round(ms_serial, 4),
                                         speedup=round(pub["ms_per_match"] / ms_per_step, 1))
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist_on:
         dist.barrier()
         dist.destroy_process_group()
 

@@ -70,3 +70,29 @@ def test_two_rank_gloo_line_has_every_field():
     v = d["verify_gather"]
     assert v["ok"] and v["slots"] >= 2 and v["bands"] == 2
     assert "frames.json" in v["check"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["cfg2", "cfg3"])
+def test_rccl_gather_rehearsal(config):
+    """The RCCL branch of the N>1 bench on the one-GPU box: a 1-rank nccl
+    process group runs the whole gather path -- the match writing its band straight into the
+    packed device buffer (int16 disparities with the NXC stage, float32 with subpixel), the
+    async RCCL gather issued from the frames' streams, the int16 landing on rank 0, the
+    gather timed with HIP events, and every gathered slot verified against the oracle's
+    whole-frame hash. What it cannot cover is the transport between distinct GPUs."""
+    p = _run(["--config", config, "--gather-rehearsal", "--steps", "3", "--warmup", "1",
+              "--spinup-ms", "0", "--no-cpu-baseline", "--kernel-reps", "0", "--no-host-path"],
+             timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["value"] > 0
+    assert "rehearsal" in d["config"]["parallelism"] and "RCCL" in d["config"]["parallelism"]
+    assert d["config"]["backend"] == "nccl"
+    g = d["gather"]
+    assert g["ms"] > 0 and g["bytes_to_root"] == 0
+    v = d["verify_gather"]
+    assert v["ok"] and v["slots"] >= 2 and v["bands"] == 1
+    assert "frames.json" in v["check"]
