@@ -683,6 +683,33 @@ def test_mx_search_edges(gpu, oracle, words, W):
         gpu.tune(0, 0, 0, 0)
 
 
+@pytest.mark.parametrize("k", [2, 4, 6])
+@pytest.mark.parametrize("W", [777, 2048, 4100])
+def test_mx_tie_only_blocks(gpu, oracle, k, W):
+    """NoDuplicates on sparse random descriptors (each bit set with p = 2^-k: small integer
+    costs, so most blocks TIE the running minimum cost without lowering it, the case the
+    paired search records with the block's own key instead of the last-minimum tree), for
+    the 2-tile pipelined kernel (few rows) and the 4-tile one (tuned), one and several LDS
+    chunks; against the oracle."""
+    H, words = 3, 4
+    rng = np.random.default_rng(W * 10 + k)
+
+    def sparse():
+        v = rng.integers(0, 2 ** 32, size=(H, W, words), dtype=np.uint64)
+        for _ in range(k - 1):
+            v &= rng.integers(0, 2 ** 32, size=(H, W, words), dtype=np.uint64)
+        return v.astype(np.uint32)
+    a, b = sparse(), sparse()
+    b[1] = a[1, np.roll(np.arange(W), 9)]  # one row with planted unique matches
+    ref = oracle.search(a, b, 1, -1)
+    try:
+        for s in [(0, 0, 0, 0), (64, 4, 8, 0), (64, 2, 8, 0)]:
+            gpu.tune(*s)
+            same(host(gpu.search(dev(_pack(a)), dev(_pack(b)), W, words, 1, -1)), ref)
+    finally:
+        gpu.tune(0, 0, 0, 0)
+
+
 @pytest.mark.parametrize("B", [129, 154, 192])
 def test_mx_search_used_bits(gpu, oracle, B):
     """256-bit descriptors whose bits >= B are zero (transform output of n = 33..49
