@@ -11,8 +11,10 @@ typedef int v8i __attribute__((ext_vector_type(8)));
 typedef float v16f __attribute__((ext_vector_type(16)));
 typedef float v4f __attribute__((ext_vector_type(4)));
 
-template <int CHAINS>
+template <int CHAINS, bool SC = false>
 __global__ __launch_bounds__(256) void k32(const int* seed, float* out, int iters) {
+    // SC: per-lane E8M0 scales from registers (the packed-key search's 2^16 / 2^0 on B)
+    const int sa = 127 + (seed[0] & 0), sb = (threadIdx.x & 32) ? 127 : 143 + (seed[1] & 0);
     const int l = threadIdx.x;
     v8i a, b;
     for (int q = 0; q < 8; ++q) {
@@ -25,7 +27,8 @@ __global__ __launch_bounds__(256) void k32(const int* seed, float* out, int iter
     for (int i = 0; i < iters; ++i)
 #pragma unroll
         for (int c = 0; c < CHAINS; ++c)
-            acc[c] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc[c], 4, 4, 0, 0, 0, 0);
+            acc[c] = SC ? __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc[c], 4, 4, 0, sa, 0, sb)
+                        : __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a, b, acc[c], 4, 4, 0, 0, 0, 0);
     float s = 0.f;
     for (int c = 0; c < CHAINS; ++c)
         for (int r = 0; r < 16; ++r) s += acc[c][r];
@@ -96,6 +99,8 @@ int main() {
         run("32x32x64", k32<1>, f32, 1, w, seed, out);
         run("32x32x64", k32<2>, f32, 2, w, seed, out);
         run("32x32x64", k32<4>, f32, 4, w, seed, out);
+        run("32x32x64 scaled", k32<1, true>, f32, 1, w, seed, out);
+        run("32x32x64 scaled", k32<4, true>, f32, 4, w, seed, out);
         run("16x16x128", k16<1>, f16, 1, w, seed, out);
         run("16x16x128", k16<4>, f16, 4, w, seed, out);
     }

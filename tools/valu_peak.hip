@@ -60,6 +60,11 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
             if (OP == 36) asm volatile("v_bfi_b32 %0, %1, %0, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
             if (OP == 37) asm volatile("v_med3_f32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
             if (OP == 38) asm volatile("v_add3_u32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
+            if (OP == 39) asm volatile("v_pk_minimum3_f16 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
+            if (OP == 40) asm volatile("v_pk_sub_u16 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 41) asm volatile("v_pk_ashrrev_i16 %0, 15, %0" : "+v"(v[c]));
+            if (OP == 42) asm volatile("v_pk_min_f16 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 43) asm volatile("v_min3_u16 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
             if (OP == 16) {  // the search loop's 128-bit mix per pair: 4 xor, 4 bcnt, lshl_or, med3, min
                 uint32_t t0, t1, t2, t3, cst, key;
                 asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t0) : "v"(v[c]), "v"(w[c]));
@@ -118,6 +123,11 @@ int main(int argc, char** argv) {
     uint32_t* out;
     hipMalloc(&out, 1 << 20);
     const int grid = p.multiProcessorCount * 8 * 4;  // 8 waves/SIMD worth of 256-thr blocks x4
+    run<39>("v_pk_minimum3_f16", out, grid);
+    run<40>("v_pk_sub_u16", out, grid);
+    run<41>("v_pk_ashrrev_i16", out, grid);
+    run<42>("v_pk_min_f16", out, grid);
+    run<43>("v_min3_u16", out, grid);
     run<30>("v_min3_f32", out, grid);
     run<31>("v_min_f32", out, grid);
     run<32>("v_max3_f32", out, grid);
