@@ -1,3 +1,8 @@
+# A/B session for one experimental library build (build/tf2.so here; edit per experiment):
+# parity subset on the experimental build, whole-frame benches interleaved with the
+# working tree's library (tools/gpu_session.sh abbench), reference kernel-bench shapes.
+# Round 3 used it for the packed-key search, the full-first reduction and the two-pixel
+# transform (profiles/pk_keys_r03.jsonl, fullfirst_r03.jsonl, transform_2px_r03.jsonl).
 set -o pipefail
 cp libbicos_amd/libbicos_amd.so build/cur.so
 cp build/tf2.so libbicos_amd/libbicos_amd.so
