@@ -216,18 +216,23 @@ extern "C" int bicos_match_bands_device(const int* devices, int ndev, const void
             if (!rc) rc = check_hip(hipSetDevice(e->device), "hipSetDevice");
             if (!rc) rc = check_hip(hipStreamWaitEvent(e->own_stream, e->ws_ready, 0), "hipStreamWaitEvent");
             if (!rc && e->device != root) {
-                // direct xGMI peer DMA into the root's maps where the link allows it
-                int can = 0;
-                if (hipDeviceCanAccessPeer(&can, e->device, root) == hipSuccess && can) {
+                // direct xGMI peer DMA into the root's maps where the link allows it, in both
+                // directions. Every step here is an optimisation: hipMemcpyPeerAsync copies
+                // between any two devices without peer access (staged by the runtime), so a
+                // refusal only costs speed and is not an error of the match. UNVERIFIED on
+                // distinct GPUs until a multi-GPU box runs tests/test_multi_gpu.py.
+                int fwd = 0, back = 0;
+                if (hipDeviceCanAccessPeer(&fwd, e->device, root) == hipSuccess && fwd &&
+                    hipDeviceCanAccessPeer(&back, root, e->device) == hipSuccess && back) {
                     const hipError_t pe = hipDeviceEnablePeerAccess(root, 0);
-                    if (pe != hipSuccess && pe != hipErrorPeerAccessAlreadyEnabled)
-                        rc = check_hip(pe, "hipDeviceEnablePeerAccess");
-                    (void)hipGetLastError();  // clear a sticky "already enabled"
+                    (void)hipGetLastError();  // clear a sticky "already enabled" / refusal
                     // peer access does not cover stream-ordered pool memory: the stage comes
                     // from this device's default pool (hipMallocAsync) and the root's maps may
                     // too, so grant each device access to the other's pool explicitly
-                    if (!rc) rc = share_pool(e->device, root);
-                    if (!rc) rc = share_pool(root, e->device);
+                    if ((pe == hipSuccess || pe == hipErrorPeerAccessAlreadyEnabled) &&
+                        share_pool(e->device, root) == 0)
+                        (void)share_pool(root, e->device);
+                    (void)hipGetLastError();
                 }
             }
             if (rc) {

@@ -80,3 +80,46 @@ def random_stack(n: int, H: int, W: int, dtype=np.uint8, seed: int = 1, maxval: 
     maxval = (255 if np.dtype(dtype) == np.uint8 else 65535) if maxval is None else maxval
     idx = np.arange(n * H * W, dtype=np.int64)
     return _uniform(idx, seed, maxval).astype(dtype).reshape(n, H, W)
+
+
+def random_descriptors(H: int, W: int, words: int, seed: int = SEED, period: int | None = None,
+                       row_begin: int = 0, row_end: int | None = None) -> np.ndarray:
+    """[rows, W, words] uint32 descriptor words for rows [row_begin, row_end) of an H x W
+    frame: word k of pixel (y, x) is the low half of splitmix64((y W + x') words + k), with
+    x' = x % period when a period is given (every minimum of a search then repeats W / period
+    times). The reference's search kernel-bench feeds random descriptors the same way
+    (bench/cuda.cu:182-256, cv::randu over the descriptor bytes)."""
+    row_end = H if row_end is None else row_end
+    ys = np.arange(row_begin, row_end, dtype=np.int64)[:, None, None]
+    xs = np.arange(W, dtype=np.int64)[None, :, None]
+    if period:
+        xs = xs % period
+    ks = np.arange(words, dtype=np.int64)[None, None, :]
+    return (splitmix64((ys * W + xs) * words + ks, seed) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
+def low_texture_stack(n: int, H: int, W: int, shift: int = 0, noise_seed: int = 1,
+                      seed: int = SEED ^ 0x10, run: int = 4, row_begin: int = 0,
+                      row_end: int | None = None) -> np.ndarray:
+    """u8 planar stack of a weakly textured scene: 8 grey levels (32 apart) constant over runs
+    of `run` columns, plus independent U{0,1,2} sensor noise per pixel (`noise_seed`). The
+    right view is the same scene moved by `shift` columns with its own noise. Neighbouring
+    columns then have near-identical descriptors, so duplicate and tied minima decide many
+    pixels (NoDuplicates keeps ~71 % at run 4, NoDuplicates|Consistency ~52 %)."""
+    row_end = H if row_end is None else row_end
+    rows = row_end - row_begin
+    out = np.empty((n, rows, W), np.uint8)
+    runs = (W - 1 + shift) // run + 1
+    cols = (np.arange(W, dtype=np.int64) + shift) // run
+    for t in range(n):
+        # level of run c of row y: top 3 bits of splitmix64((t H + y) W + c)
+        ys = np.arange(row_begin, row_end, dtype=np.int64)[:, None]
+        lv = splitmix64((t * H + ys) * W + np.arange(runs, dtype=np.int64)[None, :], seed)
+        level = (lv >> np.uint64(61)).astype(np.uint8)[:, cols]
+        # noise of pixel i = (t H + y) W + x: byte i % 8 of splitmix64(i // 8), mod 3
+        start = (t * H + row_begin) * W
+        c0, c1 = start >> 3, (start + rows * W - 1) >> 3
+        raw = splitmix64(np.arange(c0, c1 + 1, dtype=np.int64), noise_seed).view(np.uint8)
+        noise = raw[start - (c0 << 3): start - (c0 << 3) + rows * W] % np.uint8(3)
+        out[t] = level * np.uint8(32) + noise.reshape(rows, W)
+    return out

@@ -64,13 +64,49 @@ def _frames():
 
 
 def test_frames_cover_every_config():
-    from tests.golden.make_frames import FRAMES
+    from tests.golden.make_frames import FRAMES, SEARCH_FLAGS, SEARCH_FRAMES, SEARCH_SHAPE
     db = _frames()
-    assert sorted(db) == sorted(FRAMES)
-    for name, (n, H, W, cfg) in FRAMES.items():
+    assert sorted(db) == sorted(list(FRAMES) + list(SEARCH_FRAMES))
+    for name, spec in FRAMES.items():
+        n, H, W, cfg = spec[:4]
+        gen = spec[4] if len(spec) > 4 else {}
         r = db[name]
         assert (r["n"], r["H"], r["W"], r["config"]) == (n, H, W, cfg), name
+        assert (r["dtype"], r.get("maxval")) == (gen.get("dtype", "u8"), gen.get("maxval")), name
         assert len(r["disparity_bands"]) == -(-H // r["band_rows"])
+    for name, (kind, fl) in SEARCH_FRAMES.items():
+        r = db[name]
+        assert (r["H"], r["W"], r["words"]) == SEARCH_SHAPE
+        assert (r["input"], r["flags"], r["max_lr_diff"]) == (kind,) + SEARCH_FLAGS[fl]
+        assert len(r["disparity_bands"]) == -(-r["H"] // r["band_rows"])
+
+
+# Band 0 (the first 64 rows) of every round-4 fixture regenerates from the committed
+# generators + the oracle to the committed band hash (rows are independent: SURVEY.md s8 e).
+# The whole frames take minutes each; make_frames.py rebuilds them.
+@pytest.mark.parametrize("name", ["full_n6", "full_n8", "full_n12", "full_n16", "full_n8_s25",
+                                  "full_n16_s10", "cfg2_u16", "cfg3_u16"])
+def test_oracle_reproduces_frame_band0(oracle, name):
+    from tests.golden.make_frames import FRAMES, band_hashes, frame_stacks
+    rec = _frames()[name]
+    rows = rec["band_rows"]
+    L, R = frame_stacks(FRAMES[name], 0, rows)
+    d, c = oracle.match(L, R, oracle.OracleConfig(**rec["config"]))
+    assert band_hashes(d, rows)[0] == rec["disparity_bands"][0]
+    assert band_hashes(c, rows)[0] == rec["corrmap_bands"][0]
+
+
+@pytest.mark.parametrize("kind", ["random", "periodic64", "lowtex"])
+def test_oracle_reproduces_search_band0(oracle, kind):
+    from tests.golden.make_frames import SEARCH_FLAGS, band_hashes, search_inputs
+    db = _frames()
+    rows = db["search_%s_nodupes" % kind]["band_rows"]
+    d0, d1, bits = search_inputs(kind, oracle, 0, rows)
+    for fl, (flags, lr) in SEARCH_FLAGS.items():
+        rec = db["search_%s_%s" % (kind, fl)]
+        assert rec["bits"] == bits
+        d = oracle.search(d0, d1, flags, lr)
+        assert band_hashes(d, rows)[0] == rec["disparity_bands"][0], fl
 
 
 def test_oracle_reproduces_frame_cfg1(oracle):

@@ -360,11 +360,12 @@ def _frames():
     return _FRAMES
 
 
-def _frame_stacks(n, H, W):
-    key = (n, H, W)
+def _frame_stacks(n, H, W, dtype="u8", maxval=None):
+    key = (n, H, W, dtype, maxval)
     if key not in _STACKS:
         _STACKS.clear()  # one frame's stacks at a time (cfg5: 0.55 GB of host memory)
-        _STACKS[key] = stereo_stack(n, H, W)
+        _STACKS[key] = stereo_stack(n, H, W, np.uint16 if dtype == "u16" else np.uint8,
+                                    maxval=maxval)
     return _STACKS[key]
 
 
@@ -372,7 +373,7 @@ def _check_frame(gpu, oracle, name):
     from tests.golden.make_frames import band_hashes, sha
     rec = _frames()[name]
     n, H, W, cfg = rec["n"], rec["H"], rec["W"], rec["config"]
-    L, R = _frame_stacks(n, H, W)
+    L, R = _frame_stacks(n, H, W, rec.get("dtype", "u8"), rec.get("maxval"))
     assert [sha(L), sha(R)] == rec["inputs_sha256"], "synthetic generator changed"
     got_d, got_c = gpu_match(gpu, L, R, **cfg)
     assert str(got_d.dtype) == rec["disparity_dtype"]
@@ -440,6 +441,59 @@ def test_full_frame_readme(gpu, oracle):
     valid, err = _planted(got_d, 2200)
     assert valid.mean() > 0.9
     assert (err[valid] <= 1.0).all()
+
+
+# FULL mode at the reference integration bench's shape and settings (bench/cuda.cu:297-323:
+# FULL, threshold 0.9, n = 6/8/12/16, subpixel none / 0.25 / 0.1), and 16-bit stacks at the
+# cfg2 shape (12-bit camera; full 16-bit range with min-variance + subpixel)
+@pytest.mark.parametrize("name", ["full_n6", "full_n8", "full_n12", "full_n16", "full_n8_s25",
+                                  "full_n16_s10", "cfg2_u16", "cfg3_u16"])
+def test_full_frame_modes(gpu, oracle, name):
+    # every pixel is the check (the hashes); the planted disparity is recovered wherever the
+    # search keeps a pixel (FULL n = 6 keeps few: 27-bit descriptors tie often)
+    got_d, _ = _check_frame(gpu, oracle, name)
+    valid, err = _planted(got_d, _frames()[name]["H"])
+    assert valid.mean() > 0.1
+    assert (err[valid] <= 1.0).mean() > 0.95
+
+
+# The search's hard paths at size: the int16 result of bicos_search_device on 128-bit
+# descriptors at 3300x2200 (the reference kernel-bench shape) -- random, periodic-64 (every
+# minimum duplicated) and low-texture (ties decide ~30 % of pixels) -- through NODUPES,
+# CONSISTENCY and NODUPES|CONSISTENCY (max_lr_diff 3), every pixel against the oracle's hash
+_SEARCH_NAMES = ["search_%s_%s" % (i, f) for i in ("random", "periodic64", "lowtex")
+                 for f in ("nodupes", "cons", "both")]
+_SEARCH_IN = {}
+
+
+@pytest.mark.parametrize("name", _SEARCH_NAMES)
+def test_full_frame_search_inputs(gpu, oracle, name):
+    import torch
+    from tests.golden.make_frames import band_hashes, search_inputs, sha
+    rec = _frames()[name]
+    H, W, words = rec["H"], rec["W"], rec["words"]
+    if rec["input"] not in _SEARCH_IN:
+        _SEARCH_IN.clear()  # one input at a time (2 x 116 MB of descriptors)
+        d0, d1, bits = search_inputs(rec["input"], oracle)
+        assert [sha(d0), sha(d1)] == rec["inputs_sha256"], "descriptor generator changed"
+        pitch = gpu._L.bicos_desc_pitch(W, words)
+        assert pitch == W * words  # 3300 x 4 words: rows need no padding
+        _SEARCH_IN[rec["input"]] = (
+            d0, d1, torch.from_numpy(d0.view(np.int32).reshape(H, pitch)).cuda(),
+            torch.from_numpy(d1.view(np.int32).reshape(H, pitch)).cuda(), bits)
+    d0, d1, t0, t1, bits = _SEARCH_IN[rec["input"]]
+    assert bits == rec["bits"]
+    got = host(gpu.search(t0, t1, W, words, rec["flags"], rec["max_lr_diff"], bits=bits))
+    if sha(got) == rec["disparity_sha256"]:
+        return
+    bad = [i for i, (a, b) in enumerate(zip(band_hashes(got, rec["band_rows"]),
+                                            rec["disparity_bands"])) if a != b]
+    b0 = bad[0] * rec["band_rows"]
+    e0 = min(H, b0 + rec["band_rows"])
+    ref = oracle.search(d0[b0:e0], d1[b0:e0], rec["flags"], rec["max_lr_diff"])
+    same(got[b0:e0].copy(), ref)
+    raise AssertionError("%s: %d bands differ, yet rows %d-%d match the oracle" % (
+        name, len(bad), b0, e0))
 
 
 def test_row_band_sharding_is_exact(gpu):
@@ -748,20 +802,35 @@ def test_mx_is_the_default_search(gpu):
 def test_cfg5_full_size_and_bands(gpu, oracle):
     """3840x2160x33 (BASELINE cfg5) on one GPU: the whole frame against the oracle's hashes
     (tests/golden/frames.json), and the 8 row bands of 270 the 8-GPU run computes are
-    byte-identical to it."""
-    from libbicos_amd.device import MatchConfig
+    byte-identical to it -- band r matched on GPU r % device_count (distinct GPUs where the box
+    has them), then all 8 gathered onto GPU 0 by bicos_match_bands_device (peer copies)."""
+    import torch
+    from libbicos_amd.device import Engine, MatchConfig, match_bands
     from libbicos_amd.distributed import band_rows
     n, H, W = 33, 2160, 3840
-    cfg = dict(nxcorr_threshold=0.96)
+    cfg = MatchConfig(nxcorr_threshold=0.96)
     got_d, got_c = _check_frame(gpu, oracle, "cfg5")
     L, R = _frame_stacks(n, H, W)
     s0, s1 = dev(L), dev(R)
+    nd = torch.cuda.device_count()
+    engines = {0: gpu}
+    bands0, bands1 = [], []
     for r in range(8):
         b, e = band_rows(H, 8, r)
         assert e - b == 270
-        bd, bc = gpu.match(s0[:, b:e], s1[:, b:e], MatchConfig(**cfg))
+        d = r % nd
+        b0, b1 = s0[:, b:e], s1[:, b:e]
+        if d:
+            b0, b1 = b0.to("cuda:%d" % d), b1.to("cuda:%d" % d)
+            engines.setdefault(d, Engine(d))
+        bands0.append(b0)
+        bands1.append(b1)
+        bd, bc = engines[d].match(b0, b1, cfg)
         same(host(bd), got_d[b:e])
         same(host(bc), got_c[b:e])
+    gd, gc = match_bands(bands0, bands1, cfg)
+    same(host(gd), got_d)
+    same(host(gc), got_c)
     truth = (16 + (48 * np.arange(H)) // H)[:, None]
     d = got_d.astype(np.float64)
     valid = np.isfinite(d) & (d != -32768)

@@ -1,10 +1,13 @@
 """Single-process multi-GPU entries (bicos_match_host_multi, bicos_match_bands_device;
 SURVEY.md s8(e)) on the GPU box.
 
-The box has one GPU, so the bands are placed on device 0 several times: the row split, the
-per-band pipelines (threads and engines for the host form; the staged maps and the peer-copy
-gather for the device form, which every band after the first takes even on the root) and
-the reassembly are exercised exactly as on 8 GPUs; only the copies stay on one device.
+Band b runs on device b % torch.cuda.device_count() (`_devices`): on a multi-GPU box the
+bands land on distinct GPUs and the cross-device branches run (peer access, peer copies of
+the staged maps out of the stream-ordered pool, engines of different devices); on a one-GPU
+box every band is on device 0, and the row split, the per-band pipelines (threads and
+engines for the host form; the staged maps and the peer-copy gather for the device form,
+which every band after the first takes even on the root) and the reassembly are still
+exercised as on 8 GPUs, only with the copies on one device.
 The bar is byte identity with the one-GPU call, which itself is checked against the oracle
 elsewhere -- plus one direct oracle check per form.
 """
@@ -35,6 +38,28 @@ def same(a, b):
         "%d of %d elements differ" % (int((a != b).sum()), a.size)
 
 
+def _devices(k):
+    """Device of band b: round-robin over the visible GPUs (selected by count, not fixed)."""
+    import torch
+    nd = torch.cuda.device_count()
+    return [b % nd for b in range(k)]
+
+
+def _place(bands):
+    """Band b's tensor moved to device _devices(k)[b] (a slice stays a view on its own GPU)."""
+    out = []
+    for t, d in zip(bands, _devices(len(bands))):
+        out.append(t if t.device.index == d else t.to("cuda:%d" % d))
+    return out
+
+
+def test_band_devices_follow_the_device_count(gpu):
+    import torch
+    nd = torch.cuda.device_count()
+    assert _devices(9) == [b % nd for b in range(9)]
+    assert len(set(_devices(9))) == min(nd, 9)
+
+
 def _pyb_cfg(pybicos, thr=0.5, step=None, minvar=None, consistency=False, double=False):
     c = pybicos.Config()
     c.nxcorr_threshold = thr
@@ -62,7 +87,7 @@ def test_host_multi_equals_one_gpu(gpu, n, H, W, dt, kw, ndev):
     L, R = stereo_stack(n, H, W, dt)
     cfg = _pyb_cfg(pybicos, **kw)
     d1, c1 = pybicos.match(list(L), list(R), cfg)
-    dm, cm = pybicos.match(list(L), list(R), cfg, devices=[0] * ndev)
+    dm, cm = pybicos.match(list(L), list(R), cfg, devices=_devices(ndev))
     same(dm, d1)
     same(cm, c1)
 
@@ -70,7 +95,7 @@ def test_host_multi_equals_one_gpu(gpu, n, H, W, dt, kw, ndev):
 def test_host_multi_matches_oracle(gpu, oracle):
     import pybicos
     L, R = stereo_stack(33, 40, 640)
-    d, c = pybicos.match(list(L), list(R), _pyb_cfg(pybicos, thr=0.9), devices=[0, 0, 0, 0])
+    d, c = pybicos.match(list(L), list(R), _pyb_cfg(pybicos, thr=0.9), devices=_devices(4))
     rd, rc = oracle.match(L, R, oracle.OracleConfig(nxcorr_threshold=0.9))
     same(d, rd)
     same(c, rc)
@@ -107,7 +132,8 @@ def test_bands_device_equals_whole_frame(gpu, n, H, W, dt, kw, k):
     cfg = MatchConfig(**kw)
     d1, c1 = gpu.match(s0, s1, cfg)
     b = _bands(H, k)
-    dm, cm = match_bands([s0[:, r0:r1] for r0, r1 in b], [s1[:, r0:r1] for r0, r1 in b], cfg)
+    dm, cm = match_bands(_place([s0[:, r0:r1] for r0, r1 in b]),
+                         _place([s1[:, r0:r1] for r0, r1 in b]), cfg)
     same(host(dm), host(d1))
     if c1 is None:
         assert cm is None
@@ -120,7 +146,8 @@ def test_bands_device_dense_bands_and_empty_band(gpu, oracle):
     from libbicos_amd.device import MatchConfig, match_bands
     L, R = stereo_stack(33, 30, 512)
     cuts = [(0, 11), (11, 11), (11, 30)]
-    dm, cm = match_bands([dev(L[:, a:b]) for a, b in cuts], [dev(R[:, a:b]) for a, b in cuts],
+    dm, cm = match_bands(_place([dev(L[:, a:b]) for a, b in cuts]),
+                         _place([dev(R[:, a:b]) for a, b in cuts]),
                          MatchConfig(nxcorr_threshold=0.5))
     rd, rc = oracle.match(L, R, oracle.OracleConfig(nxcorr_threshold=0.5))
     same(host(dm), rd)
@@ -136,7 +163,8 @@ def test_bands_device_repeated_calls_reuse_the_stage(gpu):
         s0, s1 = dev(L), dev(R)
         d1, c1 = gpu.match(s0, s1, cfg)
         b = _bands(H, k)
-        dm, cm = match_bands([s0[:, r0:r1] for r0, r1 in b], [s1[:, r0:r1] for r0, r1 in b], cfg)
+        dm, cm = match_bands(_place([s0[:, r0:r1] for r0, r1 in b]),
+                         _place([s1[:, r0:r1] for r0, r1 in b]), cfg)
         same(host(dm), host(d1))
         same(host(cm), host(c1))
 
@@ -152,7 +180,8 @@ def test_bands_device_one_row_bands_of_narrow_frames(gpu, W, kw):
     cfg = MatchConfig(**kw)
     d1, c1 = gpu.match(s0, s1, cfg)
     b = _bands(9, 9)
-    dm, cm = match_bands([s0[:, r0:r1] for r0, r1 in b], [s1[:, r0:r1] for r0, r1 in b], cfg)
+    dm, cm = match_bands(_place([s0[:, r0:r1] for r0, r1 in b]),
+                         _place([s1[:, r0:r1] for r0, r1 in b]), cfg)
     same(host(dm), host(d1))
     if c1 is not None:
         same(host(cm), host(c1))
