@@ -454,7 +454,7 @@ def test_full_frame_modes(gpu, oracle, name):
     got_d, _ = _check_frame(gpu, oracle, name)
     valid, err = _planted(got_d, _frames()[name]["H"])
     assert valid.mean() > 0.1
-    assert (err[valid] <= 1.0).mean() > 0.95
+    assert (err[valid] <= 1.0).mean() > 0.9
 
 
 # The search's hard paths at size: the int16 result of bicos_search_device on 128-bit
