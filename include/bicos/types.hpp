@@ -29,6 +29,9 @@ typedef struct ihipStream_t* hipStream_t;
 
 namespace BICOS {
 
+// reference include/common.hpp:32
+using uint128_t = __uint128_t;
+
 template <typename T>
 constexpr T INVALID_DISP = std::numeric_limits<T>::has_quiet_NaN
                                ? std::numeric_limits<T>::quiet_NaN()
@@ -55,6 +58,12 @@ struct Consistency {
 
 using SearchVariant = std::variant<Variant::NoDuplicates, Variant::Consistency>;
 
+// The reference's CUDA-build layout (common.hpp:73-82): `precision` sits between `mode` and
+// `variant` and is always declared here (the library is compiled with it, and Config crosses
+// the API by value). A caller written for the reference's CPU build that aggregate-initialises
+// Config POSITIONALLY past `mode` must name the fields instead (`cfg.variant = ...`, or C++20
+// designated initialisers `{.nxcorr_threshold = 0.9f, .variant = ...}`): the CPU build has no
+// `precision`, so its fifth positional element is the variant. INTEGRATION.md s3.
 struct Config {
     std::optional<float> nxcorr_threshold = 0.5f;
     std::optional<float> subpixel_step = std::nullopt;

@@ -263,7 +263,7 @@ void search_mx_kernel(SearchArgs a) {
     constexpr bool PAIRS = FREE && T % 2 == 0;
 #endif
     // one pair per wave: the block loop is software-pipelined (see the FREE chunk loop)
-    constexpr bool PIPE = PAIRS && T == 2;
+    constexpr bool PIPE = PAIRS && T == 2 && KS <= 3;
     // XK full blocks: the next block's A fragments are read while this one is reduced.
     // Only where the registers allow (paired NoDuplicates tiles, <= 2 K-steps): cfg2 -1.5 %,
     // cfg5 -1 %; with 3 K-steps the extra live fragments spill inside the loop (cfg4 2.3x

@@ -83,19 +83,7 @@ def test_cpp_match_branches_bit_exact(case, oracle, tmp_path):
 REF_EXE = os.path.join(ROOT, "build", "consumer", "ref_style")
 
 
-def install_and_build_consumer(prefix, bdir, quiet=True):
-    """cmake-install the in-tree libbicos_amd.so with the reference's header layout into
-    `prefix` (CMakeLists.txt, -DBICOS_PREBUILT_LIB), then configure and build the downstream
-    project tests/cpp/consumer (find_package(BICOS) + tests/cpp/ref_style.cpp) in `bdir`."""
-    lib = os.path.join(ROOT, "libbicos_amd", "libbicos_amd.so")
-    kw = dict(check=True, capture_output=quiet)
-    subprocess.run(["cmake", "-S", ROOT, "-B", os.path.join(bdir, "pkg"),
-                    "-DBICOS_PREBUILT_LIB=" + lib, "-DCMAKE_INSTALL_PREFIX=" + prefix], **kw)
-    subprocess.run(["cmake", "--install", os.path.join(bdir, "pkg")], **kw)
-    subprocess.run(["cmake", "-S", os.path.join(ROOT, "tests", "cpp", "consumer"), "-B", bdir,
-                    "-DCMAKE_PREFIX_PATH=" + prefix], **kw)
-    subprocess.run(["cmake", "--build", bdir], **kw)
-    return os.path.join(bdir, "ref_style")
+from tools.cpp_install import install_and_build_consumer  # noqa: E402,F401
 
 
 def test_installed_tree_has_the_reference_layout_and_builds_a_reference_caller(tmp_path):
