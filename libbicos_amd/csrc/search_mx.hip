@@ -201,7 +201,7 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 // Keys stay relative to the base B of the block being reduced (shifts by the signed
 // B - B_prev); C = 768 + (8160 + col1 % 32) * 2^-14 keeps both fields in [0, 16383].
 template <int WORDS, int KSU, bool NODUPES, int T, int KEYS>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KSU >= 4 ? 3 : 4)))
 void search_mx_kernel(SearchArgs a) {
     constexpr bool FK = KEYS == 3;
     static_assert(!FK || !NODUPES, "FK keys: first minimum only");
