@@ -601,21 +601,22 @@ void bicos_engine_destroy(bicos_engine* e) {
 
 int bicos_engine_tune(bicos_engine* e, int variant, int col0_per_lane, int waves, int split) {
     if (!e) return fail(BICOS_E_ARG, "null engine");
-    if (variant >= 64 && variant <= 67) {
+    if (variant >= 64 && variant <= 68) {
         // matrix-core search (64 auto keys, 65 one product + xor keys, 66 two products, 67
-        // xor keys for first-minimum searches too, no FK keys);
+        // xor keys for first-minimum searches too, no FK keys, 68 packed keys where they
+        // apply -- the automatic choice);
         // col0_per_lane = 32-column tiles per wave
         if (col0_per_lane != 0 && col0_per_lane != 2 && col0_per_lane != 4 && col0_per_lane != 8)
-            return fail(BICOS_E_ARG, "variant 64-67: tiles per wave 2|4|8");
+            return fail(BICOS_E_ARG, "variant 64-68: tiles per wave 2|4|8");
         if (waves < 0 || waves > 8) return fail(BICOS_E_ARG, "waves 1..8");
-        if (split < 0 || split > 160) return fail(BICOS_E_ARG, "variant 64-67: split = LDS KiB 0..160");
+        if (split < 0 || split > 160) return fail(BICOS_E_ARG, "variant 64-68: split = LDS KiB 0..160");
         e->tune_variant = variant;
         e->tune_R = col0_per_lane;
         e->tune_waves = waves;
         e->tune_split = split;
         return BICOS_OK;
     }
-    if (variant != 0 && variant != 16) return fail(BICOS_E_ARG, "variant 0|16|64..67");
+    if (variant != 0 && variant != 16) return fail(BICOS_E_ARG, "variant 0|16|64..68");
     if (col0_per_lane != 0 && col0_per_lane != 2 && col0_per_lane != 4)
         return fail(BICOS_E_ARG, "col0_per_lane: 2|4 (variant 16)");
     if (waves < 0 || waves > 8) return fail(BICOS_E_ARG, "waves 1..8");

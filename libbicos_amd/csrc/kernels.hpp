@@ -91,6 +91,13 @@ struct MxGeometry {
     int fk;                 // 1: float keys with the column in the free upper half of the
                             // last K-step allowed (<= 64 ksteps - 32 used bits, cols <= 2048;
                             // search_mx.hip KEYS 3, first-minimum searches only)
+    // packed Hamming keys (search_mx.hip search_pk_kernel: NoDuplicates, <= 127 used bits,
+    // 32/64/128-bit words): used instead of the fields above when pk != 0 and the search
+    // is NoDuplicates
+    int pk;
+    int pk_T;               // 64-col0 wide tiles per wave (1, 2, 4)
+    int pk_chunk;
+    int pk_tiles_per_row;
 };
 // bits: highest used descriptor bit + 1 when the bits above are known to be zero (0 =
 // all of them)

@@ -644,6 +644,326 @@ void search_mx_kernel(SearchArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Packed Hamming keys (NoDuplicates, descriptors with <= 127 used bits, 32/64/128-bit words).
+//
+// The search above spends most of its VALU issue on the first-minimum trees: one v_min3_u32
+// per two keys, one key per accumulator register. Here every accumulator register carries
+// TWO Hamming distances, and the tree runs on gfx950's v_pk_minimum3_f16 (half rate, four
+// keys per instruction; profiles/valu_rates_r03.jsonl), so the reduction per pair halves.
+//
+// Operands: right A = 1 - 2b in {+1, -1}, left B = -(1 - 2a) / 2 in {-0.5, +0.5} (both exact
+// FP4 e2m1), so one K position contributes -(1 - 2a)(1 - 2b) / 2 and K positions sum to
+// ham - K / 2 (K = 32 WORDS, the zero bits past the used ones included: they add the same
+// -1/2 to every pair). One MFMA multiplies ONE descriptor word: the B lanes of K-half 0 hold
+// word w of col0 P, those of K-half 1 word w of col0 Q = P + 32, and the E8M0 scale of the
+// K-half-0 lanes is 2^16. With C = 2^23 + 2^16 (K/2) + 0x4B00 + K/2 every D is an integer in
+// [2^23, 2^24) (ulp 1), so
+//     bits(D) = 0x4B000000 + 2^16 ham(P, col1) + 0x4B00 + ham(Q, col1)
+// exactly: the high half is 0x4B00 + ham_P, the low half 0x4B00 + ham_Q, both positive normal
+// f16 values whose order is the order of the distances (ham <= 127 keeps each in 7 bits; the
+// partial sums of the first words stay inside [0, 127] too). WORDS MFMAs cover 32 col1 x 64
+// col0 pairs: the same matrix-core work per pair as the one-product keys.
+//
+// The keys carry no column. Per wide tile (64 col0) and block (32 col1) the tree gives the
+// block's minimum distance per col0 (both lane halves combined by one v_permlane32_swap per
+// two tiles, as in pair_reduce); against the running minimum R (packed, per col0):
+//   block > R: nothing;  block == R: a second column at the running minimum -> duplicate
+//   (tracked as M = min over blocks of (block - R), packed; 0 = tie); block < R: a new
+//   minimum: the rare branch finds its first column in the block and whether the block holds
+//   it twice ((distance, row) keys through v_perm + v_pk_min_u16, first and reversed rows),
+//   and resets M. Any block order gives the same result (a tie with a later-improved minimum
+//   is forgotten on the improvement, exactly as the reference's strict '<' scan would).
+// Columns beyond the image in the partial block are set to 0x7BFF (the largest finite f16)
+// before the tree.
+constexpr uint32_t LUT_PA = 0xAAA22A22u;  // right: bit 0 -> +1.0 (0x2), 1 -> -1.0 (0xA)
+constexpr uint32_t LUT_PB = 0x11199199u;  // left: bit 0 -> -0.5 (0x9), 1 -> +0.5 (0x1)
+constexpr int PK_SCALE_HI = 127 + 16;     // E8M0 2^16 for the K-half-0 (col0 P) lanes
+constexpr uint32_t PK_PAD = 0x7BFF7BFFu;
+constexpr int PK_MAX_BITS = 127;
+constexpr int PK_MAX_COLS = 32767;
+
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+
+// v_pk_minimum3_f16 on two packed positive f16 keys per register
+__device__ __forceinline__ uint32_t pkmin3(uint32_t a, uint32_t b, uint32_t c) {
+    const h2 x = __builtin_bit_cast(h2, a), y = __builtin_bit_cast(h2, b), z = __builtin_bit_cast(h2, c);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_minimum(__builtin_elementwise_minimum(x, y), z));
+}
+__device__ __forceinline__ uint32_t pkminu(uint32_t a, uint32_t b) {  // v_pk_min_u16
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u16x2, a),
+                                                                  __builtin_bit_cast(u16x2, b)));
+}
+__device__ __forceinline__ uint32_t pksub(uint32_t a, uint32_t b) {  // v_pk_sub_u16 (wraps)
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, a) - __builtin_bit_cast(u16x2, b));
+}
+__device__ __forceinline__ uint32_t pksign(uint32_t a) {  // 0xFFFF per field with its top bit set
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(i16x2, a) >> (short)15);
+}
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
+    return (a & mask) | (b & ~mask);
+}
+
+// minimum over the 16 packed keys of a D tile (v_pk_minimum3_f16 tree, 8 instructions)
+__device__ __forceinline__ uint32_t pk_tree(const v16f& d) {
+    auto k = [&](int r) { return fbits(d[r]); };
+    const uint32_t a0 = pkmin3(k(0), k(1), k(2)), a1 = pkmin3(k(3), k(4), k(5));
+    const uint32_t a2 = pkmin3(k(6), k(7), k(8)), a3 = pkmin3(k(9), k(10), k(11));
+    const uint32_t a4 = pkmin3(k(12), k(13), k(14));
+    return pkminu(pkmin3(a0, a1, a2), pkmin3(a3, a4, k(15)));
+}
+// (distance, row) keys of ONE distance field of a D tile, minimum over this lane half's
+// rows: low half distance * 256 + row, high half distance * 256 + (31 - row), row = (r & 3)
+// + 8 (r >> 2) (the lane half's 4h is added by the caller) -- the first and the LAST row
+// at the minimum distance in one v_pk_min_u16 tree. SEL picks the distance byte of D
+// (byte 2: ham_P, byte 0: ham_Q).
+template <uint32_t SEL>
+__device__ __forceinline__ uint32_t pk_row_keys(const v16f& d) {
+    uint32_t k[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+        const uint32_t row = (uint32_t)((r & 3) + 8 * (r >> 2));
+        // bytes: [row, ham, 31 - row, ham]
+        k[r] = __builtin_amdgcn_perm(fbits(d[r]), row | ((31u - row) << 8), SEL);
+    }
+#pragma unroll
+    for (int s = 1; s < 16; s *= 2)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2 * s) k[r] = pkminu(k[r], k[r + s]);
+    return k[0];
+}
+constexpr uint32_t PK_SEL_P = 0x06010600u;
+constexpr uint32_t PK_SEL_Q = 0x04010400u;
+
+__device__ __forceinline__ v16f mfma_pk(v4i a, v4i b, v16f c, int sb) {
+    const v8i a8 = {a[0], a[1], a[2], a[3], 0, 0, 0, 0};
+    const v8i b8 = {b[0], b[1], b[2], b[3], 0, 0, 0, 0};
+    return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 127, 0, sb);
+}
+
+// T wide tiles (64 col0 each) per wave; T = 1 or an even count (tiles reduced in pairs)
+template <int WORDS, int T>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+void search_pk_kernel(SearchArgs a) {
+    static_assert(T == 1 || T % 2 == 0, "wide tiles: 1 or pairs");
+    constexpr int NP = T == 1 ? 1 : T / 2;
+    extern __shared__ __attribute__((aligned(16))) v4i lds_mx[];  // [WORDS][chunk]
+
+    const int nwg = gridDim.x;
+    const int bid = blockIdx.x;
+    const int per_xcd = (nwg + 7) / 8;
+    int logical = (bid % 8) * per_xcd + bid / 8;
+    if (nwg % 8 != 0) logical = bid;
+    const int row = logical / a.tiles_per_row;
+    const int tile = logical % a.tiles_per_row;
+
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int h = lane >> 5;
+    const int j = lane & 31;
+    const int cols = a.cols;
+    const int chunk = a.chunk;
+    const int waves = blockDim.x >> 6;
+    const int c0_wave = (tile * waves + wave) * (T * 64);
+
+    const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
+    const uint32_t* __restrict__ row1 = a.desc1 + (size_t)row * a.desc_pitch;
+
+    // B fragments: wide tile t, word w; this lane's col0 is c0_wave + 64 t + lane (K-half h:
+    // P = lanes 0-31, Q = lanes 32-63)
+    v4i bf[T][WORDS];
+#pragma unroll
+    for (int t = 0; t < T; ++t) {
+        const int c0 = c0_wave + 64 * t + lane;
+#pragma unroll
+        for (int w = 0; w < WORDS; ++w) {
+            const uint32_t x = c0 < cols ? row0[(size_t)c0 * WORDS + w] : 0u;
+            bf[t][w] = expand_bits(x, LUT_PB);
+        }
+    }
+    const int sb = h ? 127 : PK_SCALE_HI;
+    constexpr float CBIAS = 8388608.f + 65536.f * (16 * WORDS) + (float)(0x4B00 + 16 * WORDS);
+    v16f cb;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) cb[r] = CBIAS;
+    const uint32_t hh = h ? 0x00040004u : 0u;  // the lane half's row offset, both fields
+
+    // per pair p (lanes 0-31: tile 2p, lanes 32-63: tile 2p+1; T = 1: all lanes tile 0):
+    // running minimum, tie marker, first column of the minimum
+    uint32_t R[NP], M[NP], C[NP];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        R[p] = PK_PAD;
+        M[p] = 0xFFFFFFFFu;
+        C[p] = 0u;
+    }
+    auto rrow = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; };
+
+    // one pair's block minima x (tile 2p) / y (tile 2p+1) at block base B
+    auto pair_step = [&](int p, int B, const v16f& dx, const v16f& dy) {
+#if defined(BICOS_PK_DIAG) && BICOS_PK_DIAG == 2  // timing only: MFMA skeleton
+        M[p] = pkminu(M[p], fbits(dx[0]) ^ fbits(dy[5]));
+        return;
+#endif
+        const uint32_t x = pk_tree(dx);
+        const uint32_t y = T == 1 ? x : pk_tree(dy);
+        const auto sw = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+        const uint32_t comb = pkminu(sw[0], sw[1]);
+        const uint32_t diff = pksub(comb, R[p]);
+        M[p] = pkminu(M[p], diff);
+#if defined(BICOS_PK_DIAG) && BICOS_PK_DIAG == 1  // timing only: the branch never runs
+        const bool imp = (diff & 0x80008000u) == 0x80008001u;
+#else
+        const bool imp = (diff & 0x80008000u) != 0u;
+#endif
+        if (__builtin_amdgcn_ballot_w64(imp)) {
+            // a new running minimum somewhere in the pair: per (tile, distance field) that
+            // holds one, the first row at it and whether the block holds it twice
+            const uint32_t mi = pksign(diff);
+            const uint32_t hoff = h ? 0xFFFC0004u : 0u;  // rows + 4h (low), 31 - rows - 4h (high)
+            auto field = [&](auto sel_tag, uint32_t top, int sh) {
+                constexpr uint32_t SEL = decltype(sel_tag)::value;
+                const uint64_t bal = __builtin_amdgcn_ballot_w64((diff & top) != 0u);
+                uint32_t lo = (uint32_t)bal, hi = (uint32_t)(bal >> 32);
+                asm volatile("" : "+s"(lo), "+s"(hi));
+                if (T == 1) hi = 0;  // (one tile: both halves hold it)
+                if (!(lo | hi)) return;
+                uint32_t kx = 0, ky = 0;
+                if (lo) kx = pk_row_keys<SEL>(dx) + hoff;
+                if constexpr (T != 1) {
+                    if (hi) ky = pk_row_keys<SEL>(dy) + hoff;
+                }
+                if (!lo) kx = ky;
+                if (!hi) ky = kx;
+                const auto sk = __builtin_amdgcn_permlane32_swap(kx, ky, false, false);
+                const uint32_t res = pkminu(sk[0], sk[1]);
+                const uint32_t first = res & 0x1Fu;
+                const uint32_t uniq = first + ((res >> 16) & 0x1Fu) == 31u ? 0xFFFFu : 0u;
+                const uint32_t fm = mi & (0xFFFFu << sh);
+                R[p] = bfi(fm, comb, R[p]);
+                C[p] = bfi(fm, ((uint32_t)B + first) << sh, C[p]);
+                M[p] = bfi(fm, uniq << sh, M[p]);
+            };
+            field(std::integral_constant<uint32_t, PK_SEL_P>{}, 0x80000000u, 16);
+            field(std::integral_constant<uint32_t, PK_SEL_Q>{}, 0x00008000u, 0);
+        }
+    };
+
+    const bool idle = c0_wave >= cols;  // wave-uniform; still joins the barriers
+    const int nchunks = (cols + chunk - 1) / chunk;
+    // chunks downwards from the one holding the workgroup's highest col0, blocks downwards
+    // from the wave's highest col0 (stereo matches lie at col1 <= col0 within a few blocks,
+    // so the running minimum is found early and later blocks rarely take the branch)
+    const int cstart = min(cols - 1, (tile + 1) * waves * T * 64 - 1) / chunk;
+    for (int k = 0; k < nchunks; ++k) {
+        int ci = cstart - k;
+        if (ci < 0) ci += nchunks;
+        const int base = ci * chunk;
+        const int ncols = min(chunk, cols - base);
+        if (k) __syncthreads();
+        for (int c = threadIdx.x; c < chunk; c += blockDim.x) {
+            const int c1 = base + c;
+#pragma unroll
+            for (int w = 0; w < WORDS; ++w) {
+                const uint32_t x = c1 < cols ? row1[(size_t)c1 * WORDS + w] : 0u;
+                lds_mx[w * chunk + c] = expand_bits(x, LUT_PA);
+            }
+        }
+        __syncthreads();
+        if (idle) continue;
+
+        const int nfull = ncols / 32;
+        auto block = [&](int b, bool pad) {
+            const int B = base + 32 * b;
+#if !defined(BICOS_PK_NOPIN)
+            // (C kept in VGPRs: left alone the compiler re-copies it from SGPRs every block)
+            asm volatile("" : "+v"(cb));
+#endif
+            v4i af[WORDS];
+#pragma unroll
+            for (int w = 0; w < WORDS; ++w) af[w] = lds_mx[w * chunk + 32 * b + j];
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                const int tx = T == 1 ? 0 : 2 * p, ty = T == 1 ? 0 : 2 * p + 1;
+                v16f dx = mfma_pk(af[0], bf[tx][0], cb, sb);
+                v16f dy = dx;
+                if constexpr (T != 1) dy = mfma_pk(af[0], bf[ty][0], cb, sb);
+#pragma unroll
+                for (int w = 1; w < WORDS; ++w) {
+                    dx = mfma_pk(af[w], bf[tx][w], dx, sb);
+                    if constexpr (T != 1) dy = mfma_pk(af[w], bf[ty][w], dy, sb);
+                }
+                if (pad) {
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const bool in = 32 * b + rrow(r) < ncols;
+                        dx[r] = in ? dx[r] : bitsf(PK_PAD);
+                        dy[r] = in ? dy[r] : bitsf(PK_PAD);
+                    }
+                }
+                pair_step(p, B, dx, dy);
+            }
+        };
+        if ((ncols & 31) != 0) block(nfull, true);
+        const int sb0 = max(0, min(nfull - 1, (c0_wave + 64 * T - 1 - base) / 32));
+        for (int i = 0; i < nfull; ++i) {
+            int b = sb0 - i;
+            if (b < 0) b += nfull;
+            block(b, false);
+        }
+    }
+    if (idle) return;
+
+    int16_t* out = a.out + (size_t)row * a.out_pitch;
+    int jo = j;
+    asm volatile("" : "+v"(jo));
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+        if (T == 1 && h) continue;  // one tile: lanes 0-31 hold it
+        const int t = T == 1 ? 0 : 2 * p + h;
+#pragma unroll
+        for (int f = 0; f < 2; ++f) {  // f = 0: high field (col0 P), 1: low field (Q = P + 32)
+            const int c0 = c0_wave + 64 * t + 32 * f + jo;
+            if (c0 >= cols) continue;
+            const int sh = f ? 0 : 16;
+            const int best = (int)((C[p] >> sh) & 0xFFFFu);
+            const bool ok = ((M[p] >> sh) & 0xFFFFu) != 0u;
+            int16_t v;
+            if (a.out_mode == 0)
+                v = ok ? (int16_t)(c0 - best) : INVALID_I16;
+            else
+                v = ok ? (int16_t)best : (int16_t)-1;
+            out[c0] = v;
+        }
+    }
+}
+
+template <int WORDS, int T>
+hipError_t launch_pk(const SearchArgs& a, int waves, hipStream_t st) {
+    const size_t lds = (size_t)WORDS * a.chunk * 16;
+    const auto kern = search_pk_kernel<WORDS, T>;
+    if (lds > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, dim3(a.rows * a.tiles_per_row), dim3(64 * waves), lds, st, a);
+    return hipGetLastError();
+}
+
+template <int WORDS>
+hipError_t launch_pk_w(const SearchArgs& a, const MxGeometry& g, hipStream_t st) {
+    switch (g.pk_T) {
+        case 1: return launch_pk<WORDS, 1>(a, g.waves, st);
+        case 2: return launch_pk<WORDS, 2>(a, g.waves, st);
+        case 4:
+            if constexpr (WORDS <= 2) return launch_pk<WORDS, 4>(a, g.waves, st);
+    }
+    return hipErrorInvalidValue;
+}
+
 template <int WORDS, int KSU, bool NODUPES, int T, int KEYS>
 hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     constexpr int WL = 2 * KSU;
@@ -745,6 +1065,18 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     }
     const long per_wg = 32L * g.waves * g.T;
     g.tiles_per_row = (int)((cols + per_wg - 1) / per_wg);
+    // packed keys (variant 68 only, round 4: measured per descriptor width before it is made
+    // a default anywhere): same workgroup shape, a wide tile = two 32-col0 tiles; the LDS
+    // stage holds one expanded word per descriptor word
+    g.pk = keys == 4 && bits > 0 && bits <= PK_MAX_BITS && bits <= 32 * words &&
+           (words == 1 || words == 2 || words == 4) && cols <= PK_MAX_COLS;
+    g.pk_T = g.T >= 2 ? g.T / 2 : 1;
+    if (words == 4 && g.pk_T > 2) g.pk_T = 2;  // (4 wide tiles' B fragments do not fit)
+    int pchunk = (lds_bytes / (words * 16)) & ~31;
+    if (pchunk < 32) pchunk = 32;
+    g.pk_chunk = cols32 < pchunk ? cols32 : pchunk;
+    const long pk_wg = 64L * g.waves * g.pk_T;
+    g.pk_tiles_per_row = (int)((cols + pk_wg - 1) / pk_wg);
     return g;
 }
 
@@ -753,6 +1085,17 @@ hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool n
     if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
     if (a.cols > 32767 || g.chunk < 32 || (g.chunk & 31) || g.waves < 1 || g.waves > 8)
         return hipErrorInvalidValue;
+    if (g.pk && nodupes) {
+        if (a.cols > PK_MAX_COLS || g.pk_chunk < 32 || (g.pk_chunk & 31)) return hipErrorInvalidValue;
+        a.chunk = g.pk_chunk;
+        a.tiles_per_row = g.pk_tiles_per_row;
+        switch (words) {
+            case 1: return launch_pk_w<1>(a, g, st);
+            case 2: return launch_pk_w<2>(a, g, st);
+            case 4: return launch_pk_w<4>(a, g, st);
+        }
+        return hipErrorInvalidValue;
+    }
     a.chunk = g.chunk;
     a.tiles_per_row = g.tiles_per_row;
     switch (words) {

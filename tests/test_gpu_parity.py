@@ -737,6 +737,47 @@ def test_mx_search_edges(gpu, oracle, words, W):
         gpu.tune(0, 0, 0, 0)
 
 
+# Packed Hamming keys (search_mx.hip search_pk_kernel, the default NoDuplicates search when
+# the used-bits hint is <= 127): two distances per accumulator register, no column in the
+# key, first column and in-block duplicates resolved where the running minimum drops.
+# Extreme distances (0 and `bits`), rows where every col1 ties, tie-heavy sparse rows,
+# planted matches, ragged widths, one and several LDS chunks, every wide-tile count --
+# against the oracle and the one-product search (variant 65).
+@pytest.mark.parametrize("words,bits", [(1, 27), (1, 32), (2, 61), (2, 64), (4, 99), (4, 126),
+                                        (4, 127)])
+@pytest.mark.parametrize("W", [1, 31, 33, 95, 700, 2049, 4111, 9000])
+def test_pk_search(gpu, oracle, words, bits, W):
+    H = 5
+    rng = np.random.default_rng(W * 100 + bits)
+    mask = np.zeros(words, dtype=np.uint64)
+    for w in range(words):
+        lo = 32 * w
+        mask[w] = 0 if lo >= bits else (2 ** min(32, bits - lo)) - 1
+    a = rng.integers(0, 2 ** 32, size=(H, W, words), dtype=np.uint64)
+    b = a[:, np.roll(np.arange(W), 11)] ^ (rng.random((H, W, words)) < 0.05)
+    a[0, : W // 2] = 0          # distances 0 .. bits: the extreme keys
+    b[0] = np.uint64(0xFFFFFFFF)
+    b[0, : W // 3] = 0
+    b[1] = np.uint64(0xFFFFFFFF)  # every col1 ties
+    sp = rng.integers(0, 2 ** 32, size=(2, W, words), dtype=np.uint64)
+    for _ in range(3):          # sparse bits: small distances, many ties
+        sp &= rng.integers(0, 2 ** 32, size=(2, W, words), dtype=np.uint64)
+    a[2], b[2] = sp[0], sp[1]
+    b[3] = a[3, np.maximum(np.arange(W) - 40, 0)]  # planted disparities with repeats
+    a = (a & mask).astype(np.uint32)
+    b = (b & mask).astype(np.uint32)
+    try:
+        for flags, lr in ((1, -1), (3, 1)):
+            ref = oracle.search(a, b, flags, lr)
+            for s in [(0, 0, 0, 0), (64, 2, 8, 0), (64, 4, 8, 0), (68, 8, 8, 0), (68, 4, 4, 32),
+                      (68, 2, 8, 16), (65, 4, 8, 0)]:
+                gpu.tune(*s)
+                out = host(gpu.search(dev(_pack(a)), dev(_pack(b)), W, words, flags, lr, bits=bits))
+                same(out, ref)
+    finally:
+        gpu.tune(0, 0, 0, 0)
+
+
 @pytest.mark.parametrize("k", [2, 4, 6])
 @pytest.mark.parametrize("W", [777, 2048, 4100])
 def test_mx_tie_only_blocks(gpu, oracle, k, W):
