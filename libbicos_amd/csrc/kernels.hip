@@ -893,10 +893,17 @@ hipError_t launch_agree_m(const AgreeArgs& a, hipStream_t st) {
     const bool aligned = ((uintptr_t)a.stack0 % 4 == 0) && (a.row_pitch * sz) % 4 == 0 &&
                          (a.plane_pitch * sz) % 4 == 0;
     if (aligned) {
-        // u8, n <= 33: the right samples through a per-wave LDS window as well
+        // u8, n <= 33: the right samples through a per-wave LDS window as well -- opt-in
+        // (BICOS_AGREE=win, read once) until it is measured and verified on the GPU
         if constexpr (sizeof(TIn) == 1 && MAXN <= 33) {
-            hipLaunchKernelGGL((agree_win_kernel<TPrec, MAXN>), grid, dim3(256), 0, st, a);
-            return hipGetLastError();
+            static const bool win = [] {
+                const char* v = std::getenv("BICOS_AGREE");
+                return v && std::strcmp(v, "win") == 0;
+            }();
+            if (win) {
+                hipLaunchKernelGGL((agree_win_kernel<TPrec, MAXN>), grid, dim3(256), 0, st, a);
+                return hipGetLastError();
+            }
         }
         // runtime n even for an exact bucket: with a constant n the compiler front-loads
         // the conversions and doubles the VGPRs (49 -> 100 at n = 33)

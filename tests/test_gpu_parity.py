@@ -223,6 +223,36 @@ def test_agree_disparity_patterns(gpu, oracle, n, minvar):
     same(host(corr), rc)
 
 
+# agree_win_kernel (u8, n <= 33: right samples through a per-wave LDS window of at most 20
+# dwords per plane, per-lane gathers above that): the window's width swept across that limit
+# (spread 0..23 columns within 64 pixels, every alignment of its first column), invalid
+# pixels and far outliers (gather fallback) inside otherwise narrow waves, a width that is
+# not a multiple of 4 inside a 4-byte aligned pitch (the last wave partly live)
+@pytest.mark.parametrize("n", [2, 8, 9, 16, 17, 24, 25, 33])
+def test_agree_window_spans(gpu, oracle, n):
+    import torch
+    H, W, P = 48, 1021, 1024
+    L, R = stereo_stack(n, H, W, np.uint8, dmin=20, drange=4, seed=n + 77)
+    y = np.arange(H)[:, None]
+    x = np.arange(W)[None, :]
+    raw = (20 + y % 4 + x % (y // 2 + 1)).astype(np.int16)
+    raw[5::6, ::13] = -32768                  # invalid pixels
+    raw[7::8, 100::97] = 500                  # outliers: that wave gathers per lane
+    raw[3, :] = -32768                        # a row without any match
+    raw[9, 960:] = -5                         # col1 > col0, and off the row's end
+    R[:, 1, 200:210] = 7                      # constant right samples: NaN correlations
+    buf0 = torch.zeros((n, H, P), dtype=torch.uint8, device="cuda")
+    buf1 = torch.zeros((n, H, P), dtype=torch.uint8, device="cuda")
+    buf0[:, :, :W] = dev(L)
+    buf1[:, :, :W] = dev(R)
+    for mv in (None, np.float32(2.0) * np.float32(n)):
+        rd, rc = oracle.agree(raw, L, R, 0.5, mv)
+        out, corr = gpu.agree(dev(raw), buf0[:, :, :W], buf1[:, :, :W], 0.5,
+                              None if mv is None else float(mv))
+        same(host(out), rd.astype(np.float32))
+        same(host(corr), rc)
+
+
 # n covers exact buckets and padded ones (2, 12, 25, 45, 60: slots n..MAXN-1 are exact
 # no-ops) in both loop structures (pipelined MAXN <= 40, top-of-step above); steps cover
 # 41/20/8 x values, 3 and a single x (step > 2)
