@@ -6,11 +6,13 @@ mkdir -p gpurun_out
 cp libbicos_amd/libbicos_amd.so build/cur.so
 for k in 1 2; do
 for c in ${SCS:-cfg2}; do
-for l in ${LIBS:-cur head}; do
+for spec in ${LIBS:-cur head}; do
+  # a lib may carry one environment setting: name:VAR=value
+  l=${spec%%:*}; ev=; [ "$spec" != "$l" ] && ev=${spec#*:}
   cp build/$l.so libbicos_amd/libbicos_amd.so
-  timeout -k 10 240 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline --no-host-path \
-    > gpurun_out/abb_${c}_${l}_${k}.txt 2>&1 || { cp build/cur.so libbicos_amd/libbicos_amd.so; tail -5 gpurun_out/abb_${c}_${l}_${k}.txt; exit 1; }
-  python - "$l" "$c" gpurun_out/abb_${c}_${l}_${k}.txt <<'PY'
+  env $ev timeout -k 10 240 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline --no-host-path \
+    > gpurun_out/abb_${c}_${spec//[:=]/_}_${k}.txt 2>&1 || { cp build/cur.so libbicos_amd/libbicos_amd.so; tail -5 gpurun_out/abb_${c}_${spec//[:=]/_}_${k}.txt; exit 1; }
+  python - "$spec" "$c" gpurun_out/abb_${c}_${spec//[:=]/_}_${k}.txt <<'PY'
 import json, sys
 l = json.loads(open(sys.argv[3]).read().strip().splitlines()[-1])
 h = l["roofline"]["hbm"]

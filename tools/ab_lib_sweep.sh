@@ -6,10 +6,12 @@ mkdir -p gpurun_out
 cp libbicos_amd/libbicos_amd.so build/cur.so
 for k in 1 2; do
 for c in ${SCS:-cfg2}; do
-for l in ${LIBS:-cur head}; do
+for spec in ${LIBS:-cur head}; do
+  # a lib may carry one environment setting: name:VAR=value
+  l=${spec%%:*}; ev=; [ "$spec" != "$l" ] && ev=${spec#*:}
   cp build/$l.so libbicos_amd/libbicos_amd.so
-  timeout -k 10 240 python tools/search_sweep.py --config $c --variants ${SV:-0:0:0} --rounds ${ROUNDS:-3} \
-    ${RND:+--random} > gpurun_out/abl_${c}_${l}_${k}.txt 2>&1 || { cp build/cur.so libbicos_amd/libbicos_amd.so; cat gpurun_out/abl_${c}_${l}_${k}.txt; exit 1; }
-  sed "s/^/$l /" gpurun_out/abl_${c}_${l}_${k}.txt
+  env $ev timeout -k 10 240 python tools/search_sweep.py --config $c --variants ${SV:-0:0:0} --rounds ${ROUNDS:-3} \
+    ${RND:+--random} > gpurun_out/abl_${c}_${spec//[:=]/_}_${k}.txt 2>&1 || { cp build/cur.so libbicos_amd/libbicos_amd.so; cat gpurun_out/abl_${c}_${spec//[:=]/_}_${k}.txt; exit 1; }
+  sed "s/^/$spec /" gpurun_out/abl_${c}_${spec//[:=]/_}_${k}.txt
 done; done; done
 cp build/cur.so libbicos_amd/libbicos_amd.so
