@@ -660,149 +660,6 @@ __global__ __launch_bounds__(256) void agree_lds_kernel(AgreeArgs a) {
     if (a.corrmap) ((TPrec*)a.corrmap)[o] = corr;
 }
 
-// agree_lds_kernel with the right samples staged through LDS as well (8-bit stacks, n <= 33).
-// The byte gathers at col - d are the kernel's limit (hiding the disparity load changed
-// nothing, profiles/agree_rows_r03.jsonl): n load instructions per wave, each returning 64
-// bytes. Here each wave takes the span [lo, hi] of its 64 pixels' matched columns once the
-// disparities are in; when the span fits WIN_DW dwords per plane (stereo data: 64 columns
-// plus the local disparity spread), the wave loads that window of all n right planes with
-// dword loads -- ceil(n * nd / 64) per lane, 9 instead of 33 at n = 33 -- into a wave-private
-// LDS region, and every lane reads its n samples back from there. A wave whose span is wider
-// (scattered disparities) gathers per lane exactly as agree_lds_kernel. The same bytes come
-// from HBM either way; the same arithmetic and results.
-template <typename TPrec, int MAXN>
-__global__ __launch_bounds__(256) void agree_win_kernel(AgreeArgs a) {
-    constexpr int DW = 64;                       // dwords per plane of a 256-column u8 tile
-    constexpr int WPP = 256 / DW;                // planes per pass of the workgroup
-    constexpr int PASSES = (MAXN + WPP - 1) / WPP;
-    constexpr int WIN_DW = 20;                   // window dwords per plane (80 columns)
-    constexpr int WIN_LOADS = (MAXN * WIN_DW + 63) / 64;
-    __shared__ uint32_t tile_l[MAXN * DW];
-    __shared__ uint32_t win[4][MAXN * WIN_DW];
-    int tile, row;
-    xcd_rows(tile, row);
-    const int col0 = tile * 256;
-    const int col = col0 + (int)threadIdx.x;
-    const bool live = col < a.cols;
-    const int n = a.n;
-    const uint32_t pp = (uint32_t)a.plane_pitch;
-    const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int lane = (int)threadIdx.x & 63;
-    int d = live ? (int)a.raw[(size_t)row * a.raw_pitch + col] : INVALID_I16;
-    const uint32_t range = a.stack_bytes > 0xFFFFFFFCu ? 0xFFFFFFFFu : (a.stack_bytes + 3u) & ~3u;
-    const __amdgpu_buffer_rsrc_t r0 = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<void*>(a.stack0), (short)0, (int)range, 0x00020000);
-    const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<void*>(a.stack1), (short)0, (int)range, 0x00020000);
-    // left tile (as agree_lds_kernel)
-    const int p0 = __builtin_amdgcn_readfirstlane((int)threadIdx.x / DW);
-    const uint32_t lane_b = (uint32_t)col0 + 4u * (threadIdx.x % DW);
-    uint32_t w[PASSES];
-#pragma unroll
-    for (int j = 0; j < PASSES; ++j) {
-        const int p = min(j * WPP + p0, n - 1);
-        w[j] = __builtin_amdgcn_raw_buffer_load_b32(r0, lane_b, rowoff + (uint32_t)p * pp, 0);
-    }
-    const int idx1 = col - d;
-    const bool inb = live && d != INVALID_I16 && idx1 >= 0 && idx1 < a.cols;
-    // the wave's span of matched columns: two 16-bit minima in one register (lo, 32767 - hi)
-    uint32_t span = inb ? ((uint32_t)idx1 | ((uint32_t)(32767 - idx1) << 16)) : 0xFFFFFFFFu;
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) {
-        const uint32_t o = (uint32_t)__shfl_xor((int)span, m);
-        span = __builtin_bit_cast(uint32_t, __builtin_elementwise_min(
-            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned short, span),
-            __builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned short, o)));
-    }
-    span = __builtin_amdgcn_readfirstlane(span);
-    const int lo = (int)(span & 0xFFFFu), hi = 32767 - (int)(span >> 16);
-    const int lo_b = lo & ~3;
-    const int nd = (hi >> 2) - (lo >> 2) + 1;     // dwords per plane (garbage if no match)
-    const bool use_win = lo <= hi && nd <= WIN_DW;  // wave-uniform
-    uint32_t r[MAXN];
-    uint32_t v[WIN_LOADS];
-    if (use_win) {
-        // window dword k of this lane: flat index i = lane + 64 k over [plane][dword] (clamped:
-        // the spare lanes re-read the last dword), plane = i / nd by a 16-bit reciprocal (exact
-        // for i < MAXN * WIN_DW: tests/test_div_by_n.py)
-        const int total = n * nd;
-        const uint32_t rcp = (65536u + (uint32_t)nd - 1u) / (uint32_t)nd;
-#pragma unroll
-        for (int k = 0; k < WIN_LOADS; ++k) {
-            const uint32_t i = (uint32_t)min(lane + 64 * k, total - 1);
-            const uint32_t p = (i * rcp) >> 16;
-            const uint32_t q = i - p * (uint32_t)nd;
-            v[k] = __builtin_amdgcn_raw_buffer_load_b32(
-                r1, (uint32_t)lo_b + 4u * q + p * pp, rowoff, 0);
-        }
-    } else {
-        const uint32_t c1 = inb ? (uint32_t)idx1 : 0u;
-        const StackReader<uint8_t> rd1(a.stack1, a.stack_bytes);
-#pragma unroll
-        for (int t = 0; t < MAXN; ++t) r[t] = rd1(c1, rowoff + (uint32_t)min(t, n - 1) * pp);
-    }
-#pragma unroll
-    for (int j = 0; j < PASSES; ++j) {
-        const int p = j * WPP + p0;
-        if (p < n) tile_l[p * DW + threadIdx.x % DW] = w[j];
-    }
-    if (use_win) {
-#pragma unroll
-        for (int k = 0; k < WIN_LOADS; ++k) {
-            const int i = min(lane + 64 * k, n * nd - 1);
-            win[wave][i] = v[k];
-        }
-    }
-    __syncthreads();
-    if (!live) return;
-    if (use_win) {
-        const uint8_t* wb = (const uint8_t*)win[wave] + (inb ? idx1 - lo_b : 0);
-#pragma unroll
-        for (int t = 0; t < MAXN; ++t) r[t] = wb[min(t, n - 1) * nd * 4];
-    }
-    const uint8_t* lt = (const uint8_t*)tile_l + threadIdx.x;  // plane t at lt[t * 256]
-    const size_t o = (size_t)row * a.cols + col;
-    TPrec corr = (TPrec)__builtin_nan("");
-    if (inb) {
-        uint32_t sl = 0, sr = 0;
-#pragma unroll
-        for (int t = 0; t < MAXN; ++t)
-            if (t < n) {
-                sl += lt[t * 256];
-                sr += r[t];
-                if ((t & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-            }
-        asm volatile("" ::: "memory");
-        const TPrec m0 = div_p((TPrec)sl, (TPrec)n);
-        const TPrec m1 = div_p((TPrec)sr, (TPrec)n);
-        TPrec cov = 0, v0 = 0, v1 = 0;
-#pragma unroll
-        for (int t = 0; t < MAXN; ++t)
-            if (t < n) {
-                const TPrec x0 = (TPrec)(uint32_t)lt[t * 256] - m0;
-                const TPrec x1 = (TPrec)r[t] - m1;
-                cov = fma_p(x0, x1, cov);
-                v0 = fma_p(x0, x0, v0);
-                v1 = fma_p(x1, x1, v1);
-                if ((t & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-            }
-        if (a.has_minvar && (v0 < (TPrec)a.minvar || v1 < (TPrec)a.minvar))
-            corr = (TPrec)-1;
-        else
-            corr = div_p(cov, sqrt_p(v0 * v1));
-        if (corr < (TPrec)a.threshold) d = INVALID_I16;  // NaN passes, as in the reference
-    } else {
-        d = INVALID_I16;
-    }
-    if (a.out_f32)
-        ((float*)a.out)[o] = (float)d;
-    else
-        ((int16_t*)a.out)[o] = (int16_t)d;
-    if (a.corrmap) ((TPrec*)a.corrmap)[o] = corr;
-}
-
-
 // ------------------------------------------------------------------- dispatch
 
 template <typename TIn, int WORDS, int MAXN>
@@ -893,18 +750,6 @@ hipError_t launch_agree_m(const AgreeArgs& a, hipStream_t st) {
     const bool aligned = ((uintptr_t)a.stack0 % 4 == 0) && (a.row_pitch * sz) % 4 == 0 &&
                          (a.plane_pitch * sz) % 4 == 0;
     if (aligned) {
-        // u8, n <= 33: the right samples through a per-wave LDS window as well -- opt-in
-        // (BICOS_AGREE=win, read once) until it is measured and verified on the GPU
-        if constexpr (sizeof(TIn) == 1 && MAXN <= 33) {
-            static const bool win = [] {
-                const char* v = std::getenv("BICOS_AGREE");
-                return v && std::strcmp(v, "win") == 0;
-            }();
-            if (win) {
-                hipLaunchKernelGGL((agree_win_kernel<TPrec, MAXN>), grid, dim3(256), 0, st, a);
-                return hipGetLastError();
-            }
-        }
         // runtime n even for an exact bucket: with a constant n the compiler front-loads
         // the conversions and doubles the VGPRs (49 -> 100 at n = 33)
         hipLaunchKernelGGL((agree_lds_kernel<TIn, TPrec, MAXN, false>), grid, dim3(256), 0, st, a);

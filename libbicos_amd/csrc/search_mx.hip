@@ -788,7 +788,6 @@ void search_pk_kernel(SearchArgs a) {
     v16f cb;
 #pragma unroll
     for (int r = 0; r < 16; ++r) cb[r] = CBIAS;
-    const uint32_t hh = h ? 0x00040004u : 0u;  // the lane half's row offset, both fields
 
     // per pair p (lanes 0-31: tile 2p, lanes 32-63: tile 2p+1; T = 1: all lanes tile 0):
     // running minimum, tie marker, first column of the minimum
@@ -1065,10 +1064,13 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     }
     const long per_wg = 32L * g.waves * g.T;
     g.tiles_per_row = (int)((cols + per_wg - 1) / per_wg);
-    // packed keys (variant 68 only, round 4: measured per descriptor width before it is made
-    // a default anywhere): same workgroup shape, a wide tile = two 32-col0 tiles; the LDS
-    // stage holds one expanded word per descriptor word
-    g.pk = keys == 4 && bits > 0 && bits <= PK_MAX_BITS && bits <= 32 * words &&
+    // packed keys: the default NoDuplicates search for 32/64-bit descriptors (one K-step,
+    // where the key reduction, not the matrix products, bounds the one-product search: FULL
+    // n = 6 0.63 vs 1.43 ms, n = 8 0.78 vs 0.97 ms at 3208x2200, profiles/search_integ_r04.jsonl;
+    // at 128 bits it measured slower, 0.336 vs 0.311 ms at cfg2, profiles/pk_keys_r03.jsonl),
+    // or wherever variant 68 asks for it. Same workgroup shape, a wide tile = two 32-col0
+    // tiles; the LDS stage holds one expanded word per descriptor word
+    g.pk = (keys == 4 || (keys == 0 && words <= 2)) && bits > 0 && bits <= PK_MAX_BITS && bits <= 32 * words &&
            (words == 1 || words == 2 || words == 4) && cols <= PK_MAX_COLS;
     g.pk_T = g.T >= 2 ? g.T / 2 : 1;
     if (words == 4 && g.pk_T > 2) g.pk_T = 2;  // (4 wide tiles' B fragments do not fit)

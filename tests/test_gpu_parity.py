@@ -223,11 +223,11 @@ def test_agree_disparity_patterns(gpu, oracle, n, minvar):
     same(host(corr), rc)
 
 
-# agree_win_kernel (u8, n <= 33: right samples through a per-wave LDS window of at most 20
-# dwords per plane, per-lane gathers above that): the window's width swept across that limit
-# (spread 0..23 columns within 64 pixels, every alignment of its first column), invalid
-# pixels and far outliers (gather fallback) inside otherwise narrow waves, a width that is
-# not a multiple of 4 inside a 4-byte aligned pitch (the last wave partly live)
+# agree over disparity spreads 0..23 columns within 64 pixels at every alignment of the
+# first matched column, invalid pixels and far outliers inside otherwise narrow waves, a width
+# that is not a multiple of 4 inside a 4-byte aligned pitch (the last wave partly live). Written
+# for a per-wave LDS window of the right samples (round 4, parity-green, measured slower:
+# profiles/agree_win_r04.jsonl); kept for the LDS-tile agree.
 @pytest.mark.parametrize("n", [2, 8, 9, 16, 17, 24, 25, 33])
 def test_agree_window_spans(gpu, oracle, n):
     import torch
