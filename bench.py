@@ -790,7 +790,11 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     search_bytes = rows * W * (2 * 4 * words + 2)
     mx = mx_search()
     cons = mc.get("variant", 0) == 1
-    kname = "search_mx_kernel" if mx else "search16_kernel"
+    # packed keys: the NoDuplicates search of 32/64-bit descriptors (search_mx.hip
+    # search_pk_kernel, search_mx_geometry): the same FP4 MFMA products, two distances per
+    # accumulator register
+    pk = mx and words <= 2 and not cons and 0 < ubits <= 127
+    kname = ("search_pk_kernel" if pk else "search_mx_kernel") if mx else "search16_kernel"
     cfgname = args.config
     traffic = load_traffic(kname, cfgname, rows)
     if mx:
@@ -802,6 +806,8 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
         roof = {
             "kernel": ("search_mx_kernel<%d words> x2 (forward + reverse FP4 MFMA Hamming argmin) "
                        "+ consistency_kernel" % words if cons else
+                       "search_pk_kernel<%d words> (FP4 MFMA Hamming products, two distances per "
+                       "accumulator register, v_pk_minimum3_f16 trees)" % words if pk else
                        "search_mx_kernel<%d words> (FP4 MFMA Hamming products, argmin keys in the "
                        "accumulator)" % words),
             "bound": "mfma",

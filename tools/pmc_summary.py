@@ -46,7 +46,7 @@ def main():
     agg = collections.defaultdict(lambda: collections.defaultdict(list))
     meta = {}
     for sub in sorted(os.listdir(src)):
-        m = re.match(r"(\w+?)__b(\d+)__(\w+)$", sub)
+        m = re.match(r"([\w-]+?)__b(\d+)__(\w+)$", sub)
         if not m:
             continue
         config, N = m.group(1), int(m.group(2))
