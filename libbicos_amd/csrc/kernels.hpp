@@ -32,6 +32,8 @@ struct SearchArgs {
     int chunk;              // set by launch_search
     int tiles_per_row;      // set by launch_search
     int split;              // set by launch_search: waves per col0 group scanning col1 tiles
+    int tail_col0;          // set by launch_search_mx: first col0 of the tail workgroups
+    int tail_T;             // set by launch_search_mx: their tiles per wave (0: no tail)
 };
 
 struct SearchGeometry {
@@ -94,10 +96,15 @@ struct MxGeometry {
     // packed Hamming keys (search_mx.hip search_pk_kernel: NoDuplicates, <= 127 used bits,
     // 32/64/128-bit words): used instead of the fields above when pk != 0 and the search
     // is NoDuplicates
+    // the row's last workgroup, when it would hold only a few col0: one tail workgroup per
+    // row of tail_T (< T) tiles per wave over [tail_col0, cols) (tail_T 0: none)
+    int tail_T;
+    int tail_col0;
     int pk;
     int pk_T;               // 64-col0 wide tiles per wave (1, 2, 4)
     int pk_chunk;
     int pk_tiles_per_row;
+    int pk_tail_col0;       // cols: no tail; else one workgroup per row of 1 wide tile per wave
 };
 // bits: highest used descriptor bit + 1 when the bits above are known to be zero (0 =
 // all of them)

@@ -200,7 +200,10 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 // blocks still do it). The result is exact whatever the data: the order only changes speed.
 // Keys stay relative to the base B of the block being reduced (shifts by the signed
 // B - B_prev); C = 768 + (8160 + col1 % 32) * 2^-14 keeps both fields in [0, 16383].
-template <int WORDS, int KSU, bool NODUPES, int T, int KEYS>
+//
+// A workgroup scans one row for the col0 range [c0_base + tile * waves * T * 32, + waves * T *
+// 32), c0_base = a.tail_col0 for the tail launch (launch_mx), else 0.
+template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KSU >= 4 ? 3 : 4)))
 void search_mx_kernel(SearchArgs a) {
     constexpr bool FK = KEYS == 3;
@@ -225,6 +228,7 @@ void search_mx_kernel(SearchArgs a) {
     if (nwg % 8 != 0) logical = bid;
     const int row = logical / a.tiles_per_row;
     const int tile = logical % a.tiles_per_row;
+    const int c0_base = TAIL ? a.tail_col0 : 0;
 
     const int lane = threadIdx.x & 63;
     // wave-uniform, so the block loop's indices and addresses live in SGPRs (the SALU
@@ -235,7 +239,7 @@ void search_mx_kernel(SearchArgs a) {
     const int cols = a.cols;
     const int chunk = a.chunk;
     const int waves = blockDim.x >> 6;
-    const int c0_wave = (tile * waves + wave) * (T * 32);
+    const int c0_wave = c0_base + (tile * waves + wave) * (T * 32);
 
     const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
     const uint32_t* __restrict__ row1 = a.desc1 + (size_t)row * a.desc_pitch;
@@ -392,7 +396,7 @@ void search_mx_kernel(SearchArgs a) {
     const int nchunks = (cols + chunk - 1) / chunk;
     // FREE: chunks downwards from the one holding the workgroup's highest col0
     int cstart = 0;
-    if constexpr (FREE) cstart = min(cols - 1, (tile + 1) * waves * T * 32 - 1) / chunk;
+    if constexpr (FREE) cstart = min(cols - 1, c0_base + (tile + 1) * waves * T * 32 - 1) / chunk;
     for (int k = 0; k < nchunks; ++k) {
         int ci = FREE ? cstart - k : k;
         if (ci < 0) ci += nchunks;
@@ -743,8 +747,9 @@ __device__ __forceinline__ v16f mfma_pk(v4i a, v4i b, v16f c, int sb) {
     return __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(a8, b8, c, 4, 4, 0, 127, 0, sb);
 }
 
-// T wide tiles (64 col0 each) per wave; T = 1 or an even count (tiles reduced in pairs)
-template <int WORDS, int T>
+// T wide tiles (64 col0 each) per wave; T = 1 or an even count (tiles reduced in pairs);
+// TAIL: the col0 range starts at a.tail_col0 (the tail launch, as search_mx_kernel's)
+template <int WORDS, int T, bool TAIL>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void search_pk_kernel(SearchArgs a) {
     static_assert(T == 1 || T % 2 == 0, "wide tiles: 1 or pairs");
@@ -766,7 +771,8 @@ void search_pk_kernel(SearchArgs a) {
     const int cols = a.cols;
     const int chunk = a.chunk;
     const int waves = blockDim.x >> 6;
-    const int c0_wave = (tile * waves + wave) * (T * 64);
+    const int c0_base = TAIL ? a.tail_col0 : 0;
+    const int c0_wave = c0_base + (tile * waves + wave) * (T * 64);
 
     const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
     const uint32_t* __restrict__ row1 = a.desc1 + (size_t)row * a.desc_pitch;
@@ -855,7 +861,7 @@ void search_pk_kernel(SearchArgs a) {
     // chunks downwards from the one holding the workgroup's highest col0, blocks downwards
     // from the wave's highest col0 (stereo matches lie at col1 <= col0 within a few blocks,
     // so the running minimum is found early and later blocks rarely take the branch)
-    const int cstart = min(cols - 1, (tile + 1) * waves * T * 64 - 1) / chunk;
+    const int cstart = min(cols - 1, c0_base + (tile + 1) * waves * T * 64 - 1) / chunk;
     for (int k = 0; k < nchunks; ++k) {
         int ci = cstart - k;
         if (ci < 0) ci += nchunks;
@@ -939,17 +945,32 @@ void search_pk_kernel(SearchArgs a) {
     }
 }
 
-template <int WORDS, int T>
-hipError_t launch_pk(const SearchArgs& a, int waves, hipStream_t st) {
+template <int WORDS, int T, bool TAIL>
+hipError_t launch_pk_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st) {
     const size_t lds = (size_t)WORDS * a.chunk * 16;
-    const auto kern = search_pk_kernel<WORDS, T>;
+    const auto kern = search_pk_kernel<WORDS, T, TAIL>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, dim3(a.rows * a.tiles_per_row), dim3(64 * waves), lds, st, a);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * waves), lds, st, a);
     return hipGetLastError();
+}
+
+// main launch over [0, tail_col0); the tail (one workgroup per row, one wide tile per wave)
+// over [tail_col0, cols) when the geometry asked for one (see launch_mx_tt)
+template <int WORDS, int T>
+hipError_t launch_pk(const SearchArgs& a, int waves, hipStream_t st) {
+    hipError_t e = launch_pk_grid<WORDS, T, false>(a, waves, a.rows * a.tiles_per_row, st);
+    if constexpr (T > 1) {
+        if (e == hipSuccess && a.tail_col0 < a.cols) {
+            SearchArgs t = a;
+            t.tiles_per_row = 1;
+            e = launch_pk_grid<WORDS, 1, true>(t, waves, a.rows, st);
+        }
+    }
+    return e;
 }
 
 template <int WORDS>
@@ -963,18 +984,57 @@ hipError_t launch_pk_w(const SearchArgs& a, const MxGeometry& g, hipStream_t st)
     return hipErrorInvalidValue;
 }
 
-template <int WORDS, int KSU, bool NODUPES, int T, int KEYS>
-hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
+template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL>
+hipError_t launch_mx_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st) {
     constexpr int WL = 2 * KSU;
     const size_t lds = (size_t)WL * a.chunk * 16;
-    const auto kern = search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS>;
+    const auto kern = search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, TAIL>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, dim3(a.rows * a.tiles_per_row), dim3(64 * waves), lds, st, a);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * waves), lds, st, a);
     return hipGetLastError();
+}
+
+// rows x tiles_per_row workgroups of T tiles per wave over [0, tail_col0); then, when the row's
+// last workgroup would hold only a few col0 (tail_col0 < cols), a second launch of one
+// workgroup per row with TT < T tiles per wave over [tail_col0, cols). A tail workgroup scans
+// the whole row like the others but with fewer tiles, so the remainder no longer costs a full
+// T-tile scan: 3208 columns are 3 x 1024 + 136, and the 4th workgroup of every row ran 2 of its
+// 8 waves for a full-length scan. (One heterogeneous launch would also fill the main launch's
+// last round, but hosting both tile counts in one kernel made the main path spill.)
+template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, int TT>
+hipError_t launch_mx_tt(const SearchArgs& a, int waves, hipStream_t st) {
+    hipError_t e = launch_mx_grid<WORDS, KSU, NODUPES, T, KEYS, false>(a, waves, a.rows * a.tiles_per_row, st);
+    if constexpr (TT == 0) {
+        return e;
+    } else {
+        if (e != hipSuccess) return e;
+        SearchArgs t = a;
+        t.tiles_per_row = 1;
+        return launch_mx_grid<WORDS, KSU, NODUPES, TT, KEYS, true>(t, waves, a.rows, st);
+    }
+}
+
+template <int WORDS, int KSU, bool NODUPES, int T, int KEYS>
+hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
+    // (tail tiles: 1 or 2, and fewer than the main workgroups'; KEYS 2 only -- the any-order
+    // NoDuplicates search, whose block order starts at each wave's own col0)
+    if constexpr (KEYS == 2 && T >= 2) {
+        if (a.tail_T == 1 && a.tail_col0 < a.cols) return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 1>(a, waves, st);
+    }
+    if constexpr (KEYS == 2 && T >= 4) {
+        if (a.tail_T == 2 && a.tail_col0 < a.cols) return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 2>(a, waves, st);
+    }
+    // no tail workgroups for these keys / tile counts: the main workgroups cover every col0
+    SearchArgs b = a;
+    const long per_wg = 32L * waves * T;
+    b.tiles_per_row = (int)((a.cols + per_wg - 1) / per_wg);
+    b.tail_T = 0;
+    b.tail_col0 = a.cols;
+    return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 0>(b, waves, st);
 }
 
 // Tile counts whose registers fit (checked with -Rpass-analysis=kernel-resource-usage): 8
@@ -992,6 +1052,8 @@ hipError_t launch_mx_k(const SearchArgs& a, const MxGeometry& g, hipStream_t st)
             SearchArgs b = a;
             const long per_wg = 32L * g.waves * 4;
             b.tiles_per_row = (int)((a.cols + per_wg - 1) / per_wg);
+            b.tail_T = 0;  // (the tail was sized for 8 tiles)
+            b.tail_col0 = a.cols;
             return launch_mx<WORDS, KSU, NODUPES, 4, KEYS>(b, g.waves, st);
         }
     }
@@ -1064,6 +1126,19 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     }
     const long per_wg = 32L * g.waves * g.T;
     g.tiles_per_row = (int)((cols + per_wg - 1) / per_wg);
+    // a short remainder of the row (<= 8 waves x 2 tiles, and at most half of a workgroup)
+    // goes to one tail workgroup per row with 1 or 2 tiles per wave (search_mx_kernel TT)
+    g.tail_T = 0;
+    g.tail_col0 = cols;
+    const long rem = cols % per_wg;
+    if (rem > 0 && cols > per_wg && 2 * rem <= per_wg) {
+        const int tt = rem <= 32L * g.waves ? 1 : 2;
+        if (tt < g.T && rem <= 32L * g.waves * tt) {
+            g.tail_T = tt;
+            g.tiles_per_row = (int)(cols / per_wg);
+            g.tail_col0 = (int)(cols - rem);
+        }
+    }
     // packed keys: the default NoDuplicates search for 32/64-bit descriptors (one K-step,
     // where the key reduction, not the matrix products, bounds the one-product search: FULL
     // n = 6 0.63 vs 1.43 ms, n = 8 0.78 vs 0.97 ms at 3208x2200, profiles/search_integ_r04.jsonl;
@@ -1079,6 +1154,14 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     g.pk_chunk = cols32 < pchunk ? cols32 : pchunk;
     const long pk_wg = 64L * g.waves * g.pk_T;
     g.pk_tiles_per_row = (int)((cols + pk_wg - 1) / pk_wg);
+    // the packed search's tail: one workgroup per row of one wide tile per wave
+    g.pk_tail_col0 = cols;
+    const long pk_rem = cols % pk_wg;
+    if (g.pk_T > 1 && pk_rem > 0 && cols > pk_wg && 2 * pk_rem <= pk_wg &&
+        pk_rem <= 64L * g.waves) {
+        g.pk_tiles_per_row = (int)(cols / pk_wg);
+        g.pk_tail_col0 = (int)(cols - pk_rem);
+    }
     return g;
 }
 
@@ -1091,6 +1174,8 @@ hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool n
         if (a.cols > PK_MAX_COLS || g.pk_chunk < 32 || (g.pk_chunk & 31)) return hipErrorInvalidValue;
         a.chunk = g.pk_chunk;
         a.tiles_per_row = g.pk_tiles_per_row;
+        a.tail_T = 0;
+        a.tail_col0 = g.pk_tail_col0;
         switch (words) {
             case 1: return launch_pk_w<1>(a, g, st);
             case 2: return launch_pk_w<2>(a, g, st);
@@ -1100,6 +1185,8 @@ hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool n
     }
     a.chunk = g.chunk;
     a.tiles_per_row = g.tiles_per_row;
+    a.tail_T = g.tail_T;
+    a.tail_col0 = g.tail_col0;
     switch (words) {
         case 1: return launch_mx_w<1, 1>(a, g, nodupes, st);
         case 2: return launch_mx_w<2, 1>(a, g, nodupes, st);
