@@ -1127,11 +1127,14 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     const long per_wg = 32L * g.waves * g.T;
     g.tiles_per_row = (int)((cols + per_wg - 1) / per_wg);
     // a short remainder of the row (<= 8 waves x 2 tiles, and at most half of a workgroup)
-    // goes to one tail workgroup per row with 1 or 2 tiles per wave (search_mx_kernel TT)
+    // goes to one tail workgroup per row with 1 or 2 tiles per wave (launch_mx_tt), for
+    // 4-tile main workgroups: 3208 columns readme 1.127 vs 1.254 ms, FULL n = 12 1.127 vs
+    // 1.255; behind 2-tile ones (4-K-step 256-bit, FULL n = 16) it measured slower, 2.15 vs
+    // 2.08 ms (profiles/search_tail_r04.jsonl)
     g.tail_T = 0;
     g.tail_col0 = cols;
     const long rem = cols % per_wg;
-    if (rem > 0 && cols > per_wg && 2 * rem <= per_wg) {
+    if (g.T >= 4 && rem > 0 && cols > per_wg && 2 * rem <= per_wg) {
         const int tt = rem <= 32L * g.waves ? 1 : 2;
         if (tt < g.T && rem <= 32L * g.waves * tt) {
             g.tail_T = tt;
@@ -1154,7 +1157,8 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     g.pk_chunk = cols32 < pchunk ? cols32 : pchunk;
     const long pk_wg = 64L * g.waves * g.pk_T;
     g.pk_tiles_per_row = (int)((cols + pk_wg - 1) / pk_wg);
-    // the packed search's tail: one workgroup per row of one wide tile per wave
+    // the packed search's tail: one workgroup per row of one wide tile per wave (FULL n = 6 at
+    // 3208 columns: 0.575 vs 0.66 ms, profiles/search_tail_r04.jsonl)
     g.pk_tail_col0 = cols;
     const long pk_rem = cols % pk_wg;
     if (g.pk_T > 1 && pk_rem > 0 && cols > pk_wg && 2 * pk_rem <= pk_wg &&
