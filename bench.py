@@ -217,12 +217,17 @@ def kernel_source_hash() -> str:
     return h.hexdigest()[:16]
 
 
-def load_traffic(kernel_prefix: str, config: str, rows: int):
-    """Per-launch HBM bytes (PMC FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections) of a kernel
-    from the committed profiles/pmc_r*.json entry for this config and row count, measured on
-    the current sources (kernel_source_hash). Returns {"bytes", "source"}, or {"bytes": None,
-    "why": ...} when no such profile exists."""
+def load_traffic(kernel_prefix, config: str, rows: int):
+    """HBM bytes per frame (PMC FETCH_SIZE x2 + WRITE_SIZE, gfx950 corrections) of the kernels
+    whose names start with `kernel_prefix` (a string or a tuple of them) from the committed
+    profiles/pmc_r*.json entries for this config and row count, measured on the current
+    sources (kernel_source_hash). A stage can be several dispatches per frame -- Consistency's
+    forward and reverse search, a search's tail launch (search_mx.hip launch_mx_tt) -- so each
+    kernel group's per-dispatch bytes count as often as it was dispatched per frame (frames =
+    the fewest dispatches of any kernel of the config). Returns {"bytes", "source"}, or
+    {"bytes": None, "why": ...} when no such profile exists."""
     import glob
+    prefixes = (kernel_prefix,) if isinstance(kernel_prefix, str) else tuple(kernel_prefix)
     want = kernel_source_hash()
     stale = None
     for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_r*.json")))):
@@ -230,18 +235,21 @@ def load_traffic(kernel_prefix: str, config: str, rows: int):
             d = json.load(open(f))
         except Exception:
             continue
-        for key, c in d.get("kernels", {}).items():
-            if c.get("config") != config or c.get("rows") != rows or \
-                    not c.get("kernel", "").startswith(kernel_prefix) or \
-                    "hbm_read_bytes" not in c or "hbm_write_bytes" not in c:
-                continue
-            src = os.path.relpath(f, ROOT) + " :: " + key
-            if d.get("source_sha") != want:
-                stale = stale or src
-                continue
-            return {"bytes": c["hbm_read_bytes"] + c["hbm_write_bytes"],
-                    "read_bytes": c["hbm_read_bytes"], "write_bytes": c["hbm_write_bytes"],
-                    "source": src, "source_sha": want}
+        mine = [(key, c) for key, c in d.get("kernels", {}).items()
+                if c.get("config") == config and c.get("rows") == rows and
+                "hbm_read_bytes" in c and "hbm_write_bytes" in c]
+        hits = [(key, c) for key, c in mine if c.get("kernel", "").startswith(prefixes)]
+        if not hits:
+            continue
+        src = os.path.relpath(f, ROOT) + " :: " + "; ".join(key for key, _ in hits)
+        if d.get("source_sha") != want:
+            stale = stale or src
+            continue
+        frames = min(int(c.get("dispatches", 1)) for _, c in mine) or 1
+        rd = sum(c["hbm_read_bytes"] * int(c.get("dispatches", frames)) for _, c in hits) / frames
+        wr = sum(c["hbm_write_bytes"] * int(c.get("dispatches", frames)) for _, c in hits) / frames
+        return {"bytes": rd + wr, "read_bytes": rd, "write_bytes": wr, "source": src,
+                "source_sha": want}
     return {"bytes": None, "why": ("PMC profile %s was taken on other sources" % stale) if stale
             else "no PMC profile for %s rows=%d" % (config, rows), "source_sha": want}
 
@@ -786,8 +794,11 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     tf_bytes = rows * W * (n + 4 * words)
     valid = float((raw != -32768).float().mean().item())
     ag_bytes = rows * W * (2 + 8) + rows * W * valid * 2 * n
-    # algorithmic bytes of one search launch: both descriptor bands + the int16 output
-    search_bytes = rows * W * (2 * 4 * words + 2)
+    # algorithmic bytes of the search stage: both descriptor bands + the int16 output per pass
+    # (Consistency: forward + reverse pass, then the check reads both index maps and writes
+    # the disparity, 6 B per pixel)
+    search_bytes = rows * W * (2 * 4 * words + 2) * (2 if mc.get("variant", 0) == 1 else 1) + \
+        (rows * W * 6 if mc.get("variant", 0) == 1 else 0)
     mx = mx_search()
     cons = mc.get("variant", 0) == 1
     # packed keys: the NoDuplicates search of 32/64-bit descriptors (search_mx.hip
@@ -796,7 +807,9 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     pk = mx and words <= 2 and not cons and 0 < ubits <= 127
     kname = ("search_pk_kernel" if pk else "search_mx_kernel") if mx else "search16_kernel"
     cfgname = args.config
-    traffic = load_traffic(kname, cfgname, rows)
+    # the search stage's bytes per frame: every search dispatch (tail launches, both
+    # Consistency passes) and Consistency's check kernel
+    traffic = load_traffic((kname, "consistency_kernel") if cons else kname, cfgname, rows)
     if mx:
         alg_flops, used_flops = mx_flops(rows, W, words, mc, ubits, sbits)
         achieved_tf = alg_flops / t_search / 1e12
