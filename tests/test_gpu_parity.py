@@ -767,6 +767,39 @@ def test_mx_search_edges(gpu, oracle, words, W):
         gpu.tune(0, 0, 0, 0)
 
 
+# Tail workgroups (search_mx.hip launch_mx_tt / launch_pk, round 4): a row remainder of at most
+# half a workgroup and 8 waves x 2 tiles goes to one extra workgroup per row with 1 or 2 tiles
+# per wave. Widths on either side of every selection boundary for 4-tile (per workgroup 1024
+# col0) and 8-tile (2048) main workgroups -- remainder 1, 255/256 (1 tile), 257, 512 (2 tiles),
+# 513 (no tail) -- the README width, through NoDuplicates and NoDuplicates|Consistency (both
+# passes take the tail), one-product keys (128/256-bit) and packed keys (32/64-bit, with the
+# used-bits hint), against the oracle.
+@pytest.mark.parametrize("words", [1, 2, 4, 8])
+@pytest.mark.parametrize("W", [1025, 1279, 1280, 1281, 1536, 1537, 2049, 2560, 2561, 3208])
+def test_search_tail_workgroups(gpu, oracle, words, W):
+    H = 3
+    rng = np.random.default_rng(W * 7 + words)
+    a = rng.integers(0, 2 ** 32, size=(H, W, words), dtype=np.uint64).astype(np.uint32)
+    b = a[:, np.roll(np.arange(W), 9)] ^ (rng.random((H, W, words)) < 0.03).astype(np.uint32)
+    b[1, :, :] = b[1, :1, :]    # every col1 ties
+    a[2] &= 0x0F0F0F0F          # low-entropy row: duplicates and ties everywhere
+    b[2] &= 0x0F0F0F0F
+    if words == 8:
+        a[..., 7] &= 0x7FFFFFFF
+        b[..., 7] &= 0x7FFFFFFF
+    bits = 32 * words if words <= 2 else 0
+    try:
+        for flags, lr in ((1, -1), (3, 1)):
+            ref = oracle.search(a, b, flags, lr)
+            for s in [(0, 0, 0, 0), (64, 4, 8, 0), (64, 8, 8, 0)]:
+                gpu.tune(*s)
+                out = host(gpu.search(dev(_pack(a)), dev(_pack(b)), W, words, flags, lr,
+                                      bits=bits))
+                same(out, ref)
+    finally:
+        gpu.tune(0, 0, 0, 0)
+
+
 # Packed Hamming keys (search_mx.hip search_pk_kernel, the default NoDuplicates search when
 # the used-bits hint is <= 127): two distances per accumulator register, no column in the
 # key, first column and in-block duplicates resolved where the running minimum drops.
