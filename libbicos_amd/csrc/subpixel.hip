@@ -22,6 +22,12 @@ namespace {
 template <typename TIn, typename TPrec>
 hipError_t launch_subpixel_t(const AgreeArgs& a, int depth, bool dbl, hipStream_t st) {
     const int n = a.n;
+    // exact kernels for stack depths the buckets below would pad by a quarter or more: the
+    // reference's integration bench (FULL n = 6 / 12, bench/cuda.cu:397-401) and kernel
+    // bench (n = 10, bench/cuda.cu:44)
+    if (n == 6) return launch_subpixel_m<TIn, TPrec, 6, 6>(a, st);
+    if (n == 10) return launch_subpixel_m<TIn, TPrec, 10, 10>(a, st);
+    if (n == 12) return launch_subpixel_m<TIn, TPrec, 12, 12>(a, st);
     if (n <= 8) return launch_subpixel_m<TIn, TPrec, 8, 2>(a, st);
     if (n <= 16) return launch_subpixel_m<TIn, TPrec, 16, 9>(a, st);
     if (n <= 24) return launch_subpixel_m<TIn, TPrec, 24, 17>(a, st);

@@ -256,7 +256,8 @@ def test_agree_window_spans(gpu, oracle, n):
 # n covers exact buckets and padded ones (2, 12, 25, 45, 60: slots n..MAXN-1 are exact
 # no-ops) in both loop structures (pipelined MAXN <= 40, top-of-step above); steps cover
 # 41/20/8 x values, 3 and a single x (step > 2)
-@pytest.mark.parametrize("n,dt", [(2, np.uint8), (8, np.uint8), (12, np.uint16), (16, np.uint8),
+@pytest.mark.parametrize("n,dt", [(2, np.uint8), (6, np.uint8), (8, np.uint8), (10, np.uint8),
+                                  (12, np.uint8), (12, np.uint16), (16, np.uint8),
                                   (20, np.uint8), (25, np.uint8),
                                   (33, np.uint8), (33, np.uint16), (40, np.uint8),
                                   (45, np.uint16), (60, np.uint8), (65, np.uint8)])
