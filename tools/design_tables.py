@@ -1,6 +1,6 @@
 """Regenerate the measured tables of DESIGN.md §8 from the committed bench records:
-profiles/bench_r04.jsonl (BASELINE configs) and profiles/bench_integ_r04.jsonl (the reference
-integration grid, with profiles/bench_integ_r04_before.jsonl as the "before" column). The
+profiles/bench_r04.jsonl (the 6 BASELINE configs, then the 20 lines of the reference integration
+grid, with profiles/bench_integ_r04_before.jsonl as the "before" column). The
 tables sit between <!-- BENCH_TABLE --> / <!-- INTEG_TABLE --> markers.
 
   python tools/design_tables.py
@@ -55,7 +55,7 @@ def bench_table():
 
 
 def integ_table():
-    A, B = lines("bench_integ_r04.jsonl"), lines("bench_integ_r04_before.jsonl")
+    A, B = lines("bench_r04.jsonl"), lines("bench_integ_r04_before.jsonl")
     out = ["| n (bits, set) | one match at a time, ms: no subpixel / 0.25 / 0.20 / 0.15 / 0.10 | "
            "RTX 4090 ms | × | search ms, frac (executed K / used bits) | first measurement this "
            "round: ×, search ms |", "|---|---|---|---|---|---|"]

@@ -24,6 +24,9 @@ bash tools/gpu_session.sh benchall > /dev/null || exit 1
 for c in cfg2 cfg3 cfg4 cfg5 readme cfg1; do tail -1 gpurun_out/bench_$c.txt | cut -c1-120; done
 step integ
 bash tools/integ_grid.sh gpurun_out/integ_grid.jsonl || exit 1
+# profiles/bench_r04.jsonl = the 6 BASELINE lines, then the 20 integration lines
+for c in cfg2 cfg3 cfg4 cfg5 readme cfg1; do tail -1 gpurun_out/bench_$c.txt; done > gpurun_out/bench_r04.jsonl
+cat gpurun_out/integ_grid.jsonl >> gpurun_out/bench_r04.jsonl
 step profiso
 SCS="cfg2 cfg3 cfg4 cfg5 cfg1 readme integ-n16 integ-n6 integ-n8 integ-n12" bash tools/gpu_session.sh profiso > /dev/null || exit 1
 echo done
