@@ -65,6 +65,31 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
             if (OP == 41) asm volatile("v_pk_ashrrev_i16 %0, 15, %0" : "+v"(v[c]));
             if (OP == 42) asm volatile("v_pk_min_f16 %0, %0, %1" : "+v"(v[c]) : "v"(w[c]));
             if (OP == 43) asm volatile("v_min3_u16 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "v"(w[(c + 1) % CHAINS]));
+            // round 4: 32-bit literal operands (64-bit encodings) vs SGPR / VGPR operands
+            if (OP == 44) asm volatile("v_add_f32 %0, 0x4b400000, %0" : "+v"(v[c]));
+            if (OP == 45) asm volatile("v_and_b32 %0, 0x4b0000ff, %0" : "+v"(v[c]));
+            if (OP == 46) asm volatile("v_add_f32 %0, %1, %0" : "+v"(v[c]) : "s"(seed));
+            if (OP == 47 || OP == 48) {  // the subpixel mix per (image, x step): 12 ops, 3 literal (47) or SGPR (48)
+                uint32_t a0, a1;
+                asm volatile("v_mul_f32 %0, %1, %2" : "=v"(a0) : "v"(w[c]), "v"(v[c]));
+                asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a0) : "v"(v[c]));
+                asm volatile("v_mul_f32 %0, %1, %2" : "=v"(a1) : "v"(w[(c + 1) % CHAINS]), "v"(v[c]));
+                asm volatile("v_add_f32 %0, %0, %1" : "+v"(a0) : "v"(a1));
+                asm volatile("v_add_f32 %0, %0, %1" : "+v"(a0) : "v"(w[(c + 2) % CHAINS]));
+                if (OP == 47) {
+                    asm volatile("v_add_f32 %0, 0x4b400000, %0" : "+v"(a0));
+                    asm volatile("v_and_b32 %0, 0x4b0000ff, %0" : "+v"(a0));
+                    asm volatile("v_add_f32 %0, 0xcb000000, %0" : "+v"(a0));
+                } else {
+                    asm volatile("v_add_f32 %0, %1, %0" : "+v"(a0) : "s"(0x4b400000u ^ seed));
+                    asm volatile("v_and_b32 %0, %1, %0" : "+v"(a0) : "s"(0x4b0000ffu ^ seed));
+                    asm volatile("v_add_f32 %0, %1, %0" : "+v"(a0) : "s"(0xcb000000u ^ seed));
+                }
+                asm volatile("v_add_f32 %0, %0, %1" : "+v"(w[(c + 3) % CHAINS]) : "v"(a0));
+                asm volatile("v_sub_f32 %0, %0, %1" : "+v"(a0) : "v"(w[(c + 4) % CHAINS]));
+                asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(w[(c + 5) % CHAINS]) : "v"(a0), "v"(w[(c + 6) % CHAINS]));
+                asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(w[(c + 7) % CHAINS]) : "v"(a0));
+            }
             if (OP == 16) {  // the search loop's 128-bit mix per pair: 4 xor, 4 bcnt, lshl_or, med3, min
                 uint32_t t0, t1, t2, t3, cst, key;
                 asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t0) : "v"(v[c]), "v"(w[c]));
@@ -88,7 +113,7 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
 }
 
 template <int OP>
-double run(const char* name, uint32_t* out, int grid) {
+double run(const char* name, uint32_t* out, int grid, int wps = 8) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
@@ -104,9 +129,9 @@ double run(const char* name, uint32_t* out, int grid) {
         hipEventElapsedTime(&ms, a, b);
         if (ms < best) best = ms;
     }
-    const double ops = (double)grid * 256 * ITERS * CHAINS * (OP == 16 ? 11 : 1);  // lane-ops
+    const double ops = (double)grid * 256 * ITERS * CHAINS * (OP == 16 ? 11 : OP >= 47 ? 12 : 1);  // lane-ops
     const double tops = ops / (best * 1e-3) / 1e12;
-    printf("{\"op\": \"%s\", \"lane_ops\": %.3e, \"ms\": %.4f, \"Tops\": %.2f}\n", name, ops, best, tops);
+    printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"lane_ops\": %.3e, \"ms\": %.4f, \"Tops\": %.2f}\n", name, wps, ops, best, tops);
     return tops;
 }
 
@@ -123,6 +148,20 @@ int main(int argc, char** argv) {
     uint32_t* out;
     hipMalloc(&out, 1 << 20);
     const int grid = p.multiProcessorCount * 8 * 4;  // 8 waves/SIMD worth of 256-thr blocks x4
+    if (argc > 1 && argv[1][0] == 'l') {  // "lit": literal-operand rates, at 8 and 3 waves/SIMD
+        for (int wps : {8, 3}) {
+            const int g = p.multiProcessorCount * wps * (wps == 8 ? 4 : 1);
+            run<17>("v_add_f32", out, g, wps);
+            run<44>("v_add_f32 literal", out, g, wps);
+            run<46>("v_add_f32 sgpr", out, g, wps);
+            run<8>("v_and_b32", out, g, wps);
+            run<45>("v_and_b32 literal", out, g, wps);
+            run<47>("subpixel mix 12 ops, 3 literal", out, g, wps);
+            run<48>("subpixel mix 12 ops, 3 sgpr", out, g, wps);
+        }
+        hipFree(out);
+        return 0;
+    }
     run<39>("v_pk_minimum3_f16", out, grid);
     run<40>("v_pk_sub_u16", out, grid);
     run<41>("v_pk_ashrrev_i16", out, grid);
