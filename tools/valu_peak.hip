@@ -90,6 +90,22 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
                 asm volatile("v_fmac_f32 %0, %1, %2" : "+v"(w[(c + 5) % CHAINS]) : "v"(a0), "v"(w[(c + 6) % CHAINS]));
                 asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(w[(c + 7) % CHAINS]) : "v"(a0));
             }
+            // round 4: the transform's per-bit pair (compare into an SGPR mask, add-with-carry
+            // from it) vs a VGPR-only pair (subtract, then alignbit shifts the sign bit in)
+            if (OP == 49) {
+                uint64_t m;
+                asm volatile("v_cmp_lt_u32_e64 %0, %1, %2" : "=s"(m) : "v"(w[c]), "v"(v[c]));
+                asm volatile("v_addc_co_u32_e64 %0, vcc, %0, %0, %1" : "+v"(v[c]) : "s"(m) : "vcc");
+            }
+            if (OP == 50) {
+                uint32_t d;
+                asm volatile("v_sub_u32 %0, %1, %2" : "=v"(d) : "v"(w[c]), "v"(v[c]));
+                asm volatile("v_alignbit_b32 %0, %0, %1, 31" : "+v"(v[c]) : "v"(d));
+            }
+            if (OP == 51) asm volatile("v_alignbit_b32 %0, %0, %1, 31" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 52) asm volatile("v_lshrrev_b32 %0, 31, %0" : "+v"(v[c]));
+            if (OP == 53) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(v[c]) : "v"(w[c]));
+            if (OP == 54) asm volatile("v_add_u32 %0, %1, %0" : "+v"(v[c]) : "s"(seed));
             if (OP == 16) {  // the search loop's 128-bit mix per pair: 4 xor, 4 bcnt, lshl_or, med3, min
                 uint32_t t0, t1, t2, t3, cst, key;
                 asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t0) : "v"(v[c]), "v"(w[c]));
@@ -129,7 +145,7 @@ double run(const char* name, uint32_t* out, int grid, int wps = 8) {
         hipEventElapsedTime(&ms, a, b);
         if (ms < best) best = ms;
     }
-    const double ops = (double)grid * 256 * ITERS * CHAINS * (OP == 16 ? 11 : OP >= 47 ? 12 : 1);  // lane-ops
+    const double ops = (double)grid * 256 * ITERS * CHAINS * (OP == 16 ? 11 : (OP == 47 || OP == 48) ? 12 : (OP == 49 || OP == 50) ? 2 : 1);  // lane-ops
     const double tops = ops / (best * 1e-3) / 1e12;
     printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"lane_ops\": %.3e, \"ms\": %.4f, \"Tops\": %.2f}\n", name, wps, ops, best, tops);
     return tops;
@@ -159,6 +175,12 @@ int main(int argc, char** argv) {
             run<47>("subpixel mix 12 ops, 3 literal", out, g, wps);
             run<48>("subpixel mix 12 ops, 3 sgpr", out, g, wps);
         }
+        run<49>("v_cmp_lt_u32_e64 sgpr + v_addc_co_u32_e64 (2 ops, transform bit)", out, grid);
+        run<50>("v_sub_u32 + v_alignbit_b32 (2 ops)", out, grid);
+        run<51>("v_alignbit_b32", out, grid);
+        run<52>("v_lshrrev_b32", out, grid);
+        run<53>("v_cndmask_b32 vcc", out, grid);
+        run<54>("v_add_u32 sgpr", out, grid);
         hipFree(out);
         return 0;
     }
