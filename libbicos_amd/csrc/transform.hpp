@@ -16,8 +16,10 @@ namespace {
 // the static arrays; slots t >= n are skipped by wave-uniform branches).
 //
 // Bits are pushed MSB-first into `cur` with v_cmp (-> an SGPR lane mask) + v_addc
-// (cur = 2*cur + bit): 2 full-rate VALU per bit. Each asm block issues all its compares
-// before its adds, so every mask is read >= 2 instructions after it is written (the VALU
+// (cur = 2*cur + bit): 2 VALU per bit, both half-rate with their SGPR operands (38 T
+// lane-op/s, profiles/valu_rates_r04.jsonl; a v_sub + v_alignbit form ran at 50.7 T in
+// isolation but slower in the kernel, its alignbit chain on `cur` being serial, DESIGN.md
+// s9). Each asm block issues all its compares before its adds, so every mask is read >= 2 instructions after it is written (the VALU
 // SGPR-write -> carry-read spacing hipcc itself pads with s_nop 1 on gfx950). Loop bits sit
 // at compile-time positions (t = 0, 1: 3t..3t+2; t >= 2: 6+4(t-2)..9+4(t-2)) because the
 // per-t steps are unrolled by template recursion, so the 32-bit flushes (v_bfrev back to
