@@ -564,19 +564,11 @@ def main():
     roof = kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, world,
                            ms_per_step, frames_px) if args.kernel_reps > 0 else None
 
-    # The CPU baseline runs on rank 0 after everything else (all ranks' GPU work is done);
-    # the other ranks wait on the store without spinning, so every host core is the
-    # baseline's.
+    # The CPU baseline runs at N = 1 only (one rank, after its GPU work is done, so every
+    # host core is the baseline's); N > 1 lines carry null.
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(C, args.cpu_seconds)
-    if world > 1:
-        import datetime
-        store = dist.distributed_c10d._get_default_store()
-        if rank == 0:
-            store.set("bench_cpu_baseline_done", "1")
-        else:
-            store.wait(["bench_cpu_baseline_done"], datetime.timedelta(seconds=900))
     hp = None
     if rank == 0 and world == 1 and not args.no_host_path:
         hp = host_path(C, mcfg, reps=5)

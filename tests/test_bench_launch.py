@@ -47,9 +47,10 @@ def test_failing_rank_fails_the_launch():
 @pytest.mark.gpu
 def test_two_rank_gloo_line_has_every_field():
     """The N>1 bench line is self-contained: two gloo ranks sharing the
-    box's GPU run the row-band path; rank 0's line carries the CPU baseline, the search
-    roofline with its PMC traffic lookup, the gather timed on its own, the gathered frames
-    verified against the oracle's whole-frame hash, and a "gloo rehearsal" label."""
+    box's GPU run the row-band path; rank 0's line carries the search roofline with its PMC
+    traffic lookup, the gather timed on its own, the gathered frames verified against the
+    oracle's whole-frame hash, and a "gloo rehearsal" label (the CPU baseline is an N = 1
+    field, null here)."""
     p = _run(["--gpus", "2", "--backend", "gloo", "--steps", "3", "--warmup", "1",
               "--cpu-seconds", "2", "--kernel-reps", "2", "--no-host-path"], timeout=110)
     assert p.returncode == 0, p.stderr[-3000:]
@@ -59,8 +60,7 @@ def test_two_rank_gloo_line_has_every_field():
     assert d["n_gpus"] == 2 and d["value"] > 0
     assert "gloo rehearsal" in d["config"]["parallelism"]
     assert d["config"]["rows_per_rank"] == 768
-    cpu = d["cpu_baseline"]
-    assert cpu and cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port"
+    assert d["cpu_baseline"] is None
     roof = d["roofline"]
     assert roof["bound"] == "mfma" and 0 < roof["frac"] < 1
     assert "traffic" in roof and roof["traffic_source"]
