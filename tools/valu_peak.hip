@@ -106,6 +106,7 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
             if (OP == 52) asm volatile("v_lshrrev_b32 %0, 31, %0" : "+v"(v[c]));
             if (OP == 53) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(v[c]) : "v"(w[c]));
             if (OP == 54) asm volatile("v_add_u32 %0, %1, %0" : "+v"(v[c]) : "s"(seed));
+            if (OP == 55) asm volatile("v_min3_u32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "s"(seed));
             if (OP == 16) {  // the search loop's 128-bit mix per pair: 4 xor, 4 bcnt, lshl_or, med3, min
                 uint32_t t0, t1, t2, t3, cst, key;
                 asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t0) : "v"(v[c]), "v"(w[c]));
@@ -181,6 +182,8 @@ int main(int argc, char** argv) {
         run<52>("v_lshrrev_b32", out, grid);
         run<53>("v_cndmask_b32 vcc", out, grid);
         run<54>("v_add_u32 sgpr", out, grid);
+        run<10>("v_min3_u32", out, grid);
+        run<55>("v_min3_u32 sgpr", out, grid);
         hipFree(out);
         return 0;
     }
