@@ -107,6 +107,18 @@ __global__ __launch_bounds__(256) void k(uint32_t* out, uint32_t seed) {
             if (OP == 53) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(v[c]) : "v"(w[c]));
             if (OP == 54) asm volatile("v_add_u32 %0, %1, %0" : "+v"(v[c]) : "s"(seed));
             if (OP == 55) asm volatile("v_min3_u32 %0, %0, %1, %2" : "+v"(v[c]) : "v"(w[c]), "s"(seed));
+            if (OP == 56)  // the bit pair through VCC (VOPC e32 + VOP2 add-with-carry)
+                asm volatile("v_cmp_lt_u32_e32 vcc, %1, %2\n\tv_addc_co_u32_e32 %0, vcc, %0, %0, vcc"
+                             : "+v"(v[c]) : "v"(w[c]), "v"(v[c]) : "vcc");
+            if (OP == 57) {  // 4 compares into SGPR masks, then 4 adds (the transform's push_lt<4>)
+                uint64_t m0, m1, m2, m3, j;
+                asm volatile("v_cmp_lt_u32_e64 %1, %6, %7\n\tv_cmp_lt_u32_e64 %2, %6, %8\n\t"
+                             "v_cmp_lt_u32_e64 %3, %7, %8\n\tv_cmp_lt_u32_e64 %4, %8, %6\n\t"
+                             "v_addc_co_u32_e64 %0, %5, %0, %0, %1\n\tv_addc_co_u32_e64 %0, %5, %0, %0, %2\n\t"
+                             "v_addc_co_u32_e64 %0, %5, %0, %0, %3\n\tv_addc_co_u32_e64 %0, %5, %0, %0, %4"
+                             : "+v"(v[c]), "=&s"(m0), "=&s"(m1), "=&s"(m2), "=&s"(m3), "=&s"(j)
+                             : "v"(w[c]), "v"(w[(c + 1) % CHAINS]), "v"(w[(c + 2) % CHAINS]));
+            }
             if (OP == 16) {  // the search loop's 128-bit mix per pair: 4 xor, 4 bcnt, lshl_or, med3, min
                 uint32_t t0, t1, t2, t3, cst, key;
                 asm volatile("v_xor_b32 %0, %1, %2" : "=v"(t0) : "v"(v[c]), "v"(w[c]));
@@ -146,7 +158,7 @@ double run(const char* name, uint32_t* out, int grid, int wps = 8) {
         hipEventElapsedTime(&ms, a, b);
         if (ms < best) best = ms;
     }
-    const double ops = (double)grid * 256 * ITERS * CHAINS * (OP == 16 ? 11 : (OP == 47 || OP == 48) ? 12 : (OP == 49 || OP == 50) ? 2 : 1);  // lane-ops
+    const double ops = (double)grid * 256 * ITERS * CHAINS * (OP == 16 ? 11 : (OP == 47 || OP == 48) ? 12 : (OP == 49 || OP == 50 || OP == 56) ? 2 : OP == 57 ? 8 : 1);  // lane-ops
     const double tops = ops / (best * 1e-3) / 1e12;
     printf("{\"op\": \"%s\", \"waves_per_simd\": %d, \"lane_ops\": %.3e, \"ms\": %.4f, \"Tops\": %.2f}\n", name, wps, ops, best, tops);
     return tops;
@@ -184,6 +196,8 @@ int main(int argc, char** argv) {
         run<54>("v_add_u32 sgpr", out, grid);
         run<10>("v_min3_u32", out, grid);
         run<55>("v_min3_u32 sgpr", out, grid);
+        run<56>("v_cmp_lt_u32_e32 vcc + v_addc_co_u32_e32 vcc (2 ops)", out, grid);
+        run<57>("4 x v_cmp_lt_u32_e64 sgpr, then 4 x v_addc_co_u32_e64 (8 ops, push_lt<4>)", out, grid);
         hipFree(out);
         return 0;
     }
