@@ -35,6 +35,7 @@
 #include <stdint.h>
 
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <type_traits>
 
@@ -958,6 +959,22 @@ hipError_t launch_pk_grid(const SearchArgs& a, int waves, int nwg, hipStream_t s
     return hipGetLastError();
 }
 
+// The tail launch's shape: one workgroup per row with only the waves its columns need
+// (cols_per_wave each) and a small LDS chunk, so several tail workgroups stay resident per CU
+// (the main launch's 64 KiB chunks allow two) -- the tail rows then run in < 2 rounds of
+// workgroups instead of 4 (BICOS_TAIL_CHUNK = 0 keeps the main launch's shape; 512 vs 256 vs
+// 0: profiles/search_tail_shape_r04.jsonl).
+#ifndef BICOS_TAIL_CHUNK
+#define BICOS_TAIL_CHUNK 512
+#endif
+inline void tail_shape(SearchArgs& t, int& waves, int cols_per_wave) {
+    t.tiles_per_row = 1;
+    if (BICOS_TAIL_CHUNK <= 0) return;
+    const int rem = t.cols - t.tail_col0;
+    waves = std::max(1, std::min(waves, (rem + cols_per_wave - 1) / cols_per_wave));
+    t.chunk = std::min(t.chunk, (int)BICOS_TAIL_CHUNK);
+}
+
 // main launch over [0, tail_col0); the tail (one workgroup per row, one wide tile per wave)
 // over [tail_col0, cols) when the geometry asked for one (see launch_mx_tt)
 template <int WORDS, int T>
@@ -966,8 +983,9 @@ hipError_t launch_pk(const SearchArgs& a, int waves, hipStream_t st) {
     if constexpr (T > 1) {
         if (e == hipSuccess && a.tail_col0 < a.cols) {
             SearchArgs t = a;
-            t.tiles_per_row = 1;
-            e = launch_pk_grid<WORDS, 1, true>(t, waves, a.rows, st);
+            int tw = waves;
+            tail_shape(t, tw, 64);
+            e = launch_pk_grid<WORDS, 1, true>(t, tw, a.rows, st);
         }
     }
     return e;
@@ -1013,8 +1031,9 @@ hipError_t launch_mx_tt(const SearchArgs& a, int waves, hipStream_t st) {
     } else {
         if (e != hipSuccess) return e;
         SearchArgs t = a;
-        t.tiles_per_row = 1;
-        return launch_mx_grid<WORDS, KSU, NODUPES, TT, KEYS, true>(t, waves, a.rows, st);
+        int tw = waves;
+        tail_shape(t, tw, 32 * TT);
+        return launch_mx_grid<WORDS, KSU, NODUPES, TT, KEYS, true>(t, tw, a.rows, st);
     }
 }
 
