@@ -169,16 +169,19 @@ def mx_ksteps(words: int, bits: int) -> int:
     return ks
 
 
-def mx_flops(rows: int, W: int, words: int, cfg: dict, bits: int = 0, set_bits: int = 0):
+def mx_flops(rows: int, W: int, words: int, cfg: dict, bits: int = 0, set_bits: int = 0,
+             reverse_col1: float | None = None):
     """(algorithmic, used-bit) FLOPs of the matrix-core search per launch. Each Hamming pair
     is a K-long dot product (2K FLOPs). Algorithmic K = the descriptor bits the kernel
     multiplies: the descriptor type's width (128 for u128, the reference's popcount width),
     or fewer when whole 64-bit K-steps above the used bits are skipped (cfg4: 192 of 256;
     mx_ksteps) -- never more than executed. Used-bit K = the bits the transform actually
     sets (4n-6 LIMITED: 126 at n = 33, 154 at n = 40), the stricter view. Consistency runs
-    the forward and the reverse search."""
-    passes = 2 if cfg.get("variant", 0) == 1 else 1
-    pairs = search_pairs(rows, W, cfg) * passes
+    the forward search and the reverse search over the `reverse_col1` distinct col1 the
+    forward search kept (engine.cpp reverse_search; every col1 when None)."""
+    pairs = search_pairs(rows, W, cfg)
+    if cfg.get("variant", 0) == 1:
+        pairs += float(reverse_col1 if reverse_col1 is not None else rows * W) * W
     k_exec = min(32 * words, 64 * mx_ksteps(words, bits))
     k_used = min(k_exec, set_bits) if set_bits else k_exec
     return pairs * 2 * k_exec, pairs * 2 * k_used
@@ -190,6 +193,19 @@ def transform_bits(n: int, mode: int) -> int:
     if mode:
         return n * n - 2 * n + 3
     return 4 * n - 6 if n >= 4 else (7 if n == 3 else 4)
+
+
+def pk_key_pair_peak() -> float:
+    """Issue bound in pairs/s of the packed-key search's VALU key reduction (search_mx.hip
+    search_pk_kernel) at the measured rates. Per wide tile (64 col0) and block (32 col1),
+    2048 pairs, every lane issues the pk_tree (7 v_pk_minimum3_f16 + 1 v_pk_min_u16) and its
+    share of the pair step (v_permlane32_swap, v_pk_min_u16, v_pk_sub_u16, v_pk_min_u16 per
+    two tiles: 2 half-rate ops per tile) -- 10 half-rate instructions -- plus the tie / drop
+    test (v_and + v_cmp per two tiles: 1 full-rate); the rare new-minimum branch is not
+    counted. Per pair: 10 x 64 / 2048 half-rate and 64 / 2048 full-rate lane-ops."""
+    half = 10.0 * 64 / 2048
+    full = 1.0 * 64 / 2048
+    return 1.0 / (full / (VALU_FULL_TOPS * 1e12) + half / (VALU_HALF_TOPS * 1e12))
 
 
 def mx_key_pair_peak(words: int, cfg: dict) -> float:
@@ -334,6 +350,12 @@ def main():
     ap.add_argument("--band-of", type=int, default=1,
                     help="one process, band 0 of an N-way row split (no gather): the band a "
                          "rank of an N-GPU run computes, for profiling at band sizes")
+    ap.add_argument("--root-load", default=None, choices=["kernel", "dma"],
+                    help="with --band-of N: rehearse rank 0's gather ingress on one GPU -- per "
+                         "step, on a side stream, the N-1 other bands' packed maps are written "
+                         "into a root buffer, by a CU copy kernel (RCCL's receive runs on the "
+                         "root's CUs) or by the DMA engine (a pinned-host upload; PCIe-rate, so "
+                         "at most one in flight). Reports the band's rate under that load.")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` without torchrun: start the N ranks ourselves, before
@@ -469,6 +491,35 @@ def main():
                 frame_disps[i].copy_(disp_view(recv_all[i]))
     state = {"k": 0}
 
+    # --root-load: the bytes rank 0 of an N-way run receives per step (the other bands'
+    # packed [disparity | corrmap] buffers: 6 B/px with int16 disparities, 8 with subpixel)
+    load = None
+    if args.root_load:
+        if args.band_of < 2 or world != 1:
+            raise SystemExit("--root-load rehearses rank 0 of --band-of N (one process)")
+        bpp = (2 if (i16 or not has_corr) else 4) + (4 if has_corr else 0)
+        ing = (args.band_of - 1) * band_height(H, args.band_of) * W * bpp
+        ing = (ing + 3) // 4 * 4
+        load = {"mode": args.root_load, "bytes_per_step": ing, "issued": 0, "skipped": 0,
+                "dst": torch.empty(ing // 4, dtype=torch.int32, device=dev),
+                "src": (torch.ones(ing // 4, dtype=torch.int32, device=dev)
+                        if args.root_load == "kernel" else
+                        torch.ones(ing // 4, dtype=torch.int32).pin_memory()),
+                "stream": torch.cuda.Stream(dev), "ev": torch.cuda.Event()}
+
+    def issue_load():
+        # one ingress per step; the DMA form (PCIe-rate) skips a step while the last is busy
+        if load["issued"] and not load["ev"].query():
+            load["skipped"] += 1
+            return
+        with torch.cuda.stream(load["stream"]):
+            if load["mode"] == "kernel":
+                torch.bitwise_or(load["src"], 0, out=load["dst"])  # a CU kernel: read + write
+            else:
+                load["dst"].copy_(load["src"], non_blocking=True)  # hipMemcpyAsync H2D: SDMA
+            load["ev"].record(load["stream"])
+        load["issued"] += 1
+
     def step():
         k = state["k"]
         state["k"] += 1
@@ -476,6 +527,8 @@ def main():
         with torch.cuda.stream(streams[f]):
             if not gather:
                 engines[f].match(s0, s1, mcfg, out=outs[f], corrmap=corrs[f])
+                if load is not None and state.get("timed"):
+                    issue_load()
                 return
             i = k % NB
             if pending[i] is not None:
@@ -518,6 +571,7 @@ def main():
     warm_ms = (time.perf_counter() - t_warm) * 1e3
     if world > 1:
         dist.barrier()
+    state["timed"] = True
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -612,6 +666,15 @@ def main():
             },
             "roofline": roof,
             "gather": gather_info,
+            "root_load": None if load is None else {
+                "mode": load["mode"], "bytes_per_step": load["bytes_per_step"],
+                "loads_issued": load["issued"], "steps_skipped": load["skipped"],
+                "ingress_GBps": round(load["bytes_per_step"] * load["issued"] / elapsed / 1e9, 1),
+                "what": "rank 0's gather ingress of an N = %d run rehearsed on one GPU: the other "
+                        "%d bands' packed maps written per step into a root buffer on a side "
+                        "stream (%s)" % (args.band_of, args.band_of - 1,
+                                         "CU copy kernel" if load["mode"] == "kernel" else
+                                         "DMA engine, pinned-host upload at PCIe rate")},
             "verify_gather": verify,
             "cpu_baseline": cpu,
             "host_path": hp,
@@ -761,7 +824,21 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
         eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw, bits=ubits)
 
     reps = args.kernel_reps
+    thr = mc.get("nxcorr_threshold")
     search_launch()  # warm
+    # In the frame: the stages one after another as match_device issues them
+    # -- both transforms, the search, the agree / subpixel -- with events around the search
+    # only, so it meets the caches and clocks the frame leaves it; then back to back.
+    fe = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for a, b in fe:
+        eng.transform(s0, mcfg.mode, words, out=d0)
+        eng.transform(s1, mcfg.mode, words, out=d1)
+        a.record(st)
+        search_launch()
+        b.record(st)
+        if thr is not None:
+            eng.agree(raw, s0, s1, thr, minvar_scaled=mv, step=mc.get("subpixel_step"))
     ev[0].record(st)
     for _ in range(reps):
         search_launch()
@@ -769,7 +846,6 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     for _ in range(reps):
         eng.transform(s0, mcfg.mode, words, out=d0)
     ev[2].record(st)
-    thr = mc.get("nxcorr_threshold")
     stage = "subpixel" if mc.get("subpixel_step") else "nxcorr"
     ev[3].record(st)
     for _ in range(reps):
@@ -777,7 +853,9 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
                   step=mc.get("subpixel_step"))
     ev[4].record(st)
     torch.cuda.synchronize(dev)
-    t_search = ev[0].elapsed_time(ev[1]) / reps * 1e-3
+    t_b2b = ev[0].elapsed_time(ev[1]) / reps * 1e-3
+    in_frame = sorted(a.elapsed_time(b) * 1e-3 for a, b in fe)
+    t_search = sum(in_frame) / len(in_frame)  # the in-frame average: the reported figure
     t_tf = ev[1].elapsed_time(ev[2]) / reps * 1e-3
     t_agree = ev[3].elapsed_time(ev[4]) / reps * 1e-3
     pairs = search_pairs(rows, W, mc)
@@ -793,33 +871,63 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
         (rows * W * 6 if mc.get("variant", 0) == 1 else 0)
     mx = mx_search()
     cons = mc.get("variant", 0) == 1
-    # packed keys: the NoDuplicates search of 32/64-bit descriptors (search_mx.hip
-    # search_pk_kernel, search_mx_geometry): the same FP4 MFMA products, two distances per
-    # accumulator register
-    pk = mx and words <= 2 and not cons and 0 < ubits <= 127
+    nodupes = not cons or bool(mc.get("no_dupes", False))
+    # packed keys: the NoDuplicates search of 32/64-bit descriptors, Consistency's with
+    # no_dupes too (search_mx.hip search_pk_kernel, search_mx_geometry; ADVICE r04: the
+    # engine's own condition): the same FP4 MFMA products, two distances per register
+    pk = mx and nodupes and words <= 2
     kname = ("search_pk_kernel" if pk else "search_mx_kernel") if mx else "search16_kernel"
     cfgname = args.config
     # the search stage's bytes per frame: every search dispatch (tail launches, both
-    # Consistency passes) and Consistency's check kernel
-    traffic = load_traffic((kname, "consistency_kernel") if cons else kname, cfgname, rows)
+    # Consistency passes, the reverse list) and Consistency's check kernel
+    traffic = load_traffic((kname, "consistency_kernel", "reverse_list_kernel") if cons else kname,
+                           cfgname, rows)
+    # Consistency: the distinct col1 the forward search keeps, over which the reverse search
+    # runs (engine.cpp reverse_search)
+    kept = None
+    if cons and mx:
+        fwd = torch.empty_like(raw)
+        eng.search(d0, d1, W, words, 1 if nodupes else 0, -1, out=fwd, bits=ubits)
+        c0 = torch.arange(W, device=dev, dtype=torch.int64).expand(rows, W)
+        ok = fwd != -32768
+        mark = torch.zeros((rows, W + 1), dtype=torch.bool, device=dev)
+        mark.scatter_(1, torch.where(ok, c0 - fwd.long(), torch.full_like(c0, W)), True)
+        kept = float(mark[:, :W].sum().item())
     if mx:
-        alg_flops, used_flops = mx_flops(rows, W, words, mc, ubits, sbits)
+        alg_flops, used_flops = mx_flops(rows, W, words, mc, ubits, sbits, reverse_col1=kept)
         achieved_tf = alg_flops / t_search / 1e12
-        kpeak = mx_key_pair_peak(words, mc) / 1e9
-        evaluated = pairs * (2 if cons else 1)
+        kpeak = (pk_key_pair_peak() if pk else mx_key_pair_peak(words, mc)) / 1e9
+        evaluated = pairs + (kept if kept is not None else pairs / W) * W if cons else pairs
         k_exec = int(round(alg_flops / (2 * evaluated)))
+        fp4 = {"achieved": round(achieved_tf, 1), "peak": MFMA_FP4_DENSE_TFLOPS, "unit": "TFLOP/s",
+               "frac": round(achieved_tf / MFMA_FP4_DENSE_TFLOPS, 4)}
+        kview = {"achieved": round(evaluated / t_search / 1e9, 1), "peak": round(kpeak, 1),
+                 "unit": "Gpairs/s", "frac": round(evaluated / t_search / 1e9 / kpeak, 4)}
+        kname_long = (("search_pk_kernel<%d words> x2 (forward + reverse over the kept col1) + "
+                       "reverse_list_kernel + consistency_kernel" if pk else
+                       "search_mx_kernel<%d words> x2 (forward + reverse FP4 MFMA Hamming argmin "
+                       "over the kept col1) + reverse_list_kernel + consistency_kernel") % words
+                      if cons else
+                      "search_pk_kernel<%d words> (FP4 MFMA Hamming products, two distances per "
+                      "accumulator register, v_pk_minimum3_f16 trees)" % words if pk else
+                      "search_mx_kernel<%d words> (FP4 MFMA Hamming products, argmin keys in the "
+                      "accumulator)" % words)
+        # the packed-key search is bound by its VALU key reduction (ADVICE / VERDICT r04): its
+        # line names that bound, with the FP4 view beside it; the one-product search is
+        # co-bound and reported against the dense FP4 peak
+        main = dict(kview, bound="valu") if pk else dict(fp4, bound="mfma")
         roof = {
-            "kernel": ("search_mx_kernel<%d words> x2 (forward + reverse FP4 MFMA Hamming argmin) "
-                       "+ consistency_kernel" % words if cons else
-                       "search_pk_kernel<%d words> (FP4 MFMA Hamming products, two distances per "
-                       "accumulator register, v_pk_minimum3_f16 trees)" % words if pk else
-                       "search_mx_kernel<%d words> (FP4 MFMA Hamming products, argmin keys in the "
-                       "accumulator)" % words),
-            "bound": "mfma",
-            "achieved": round(achieved_tf, 1),
-            "peak": MFMA_FP4_DENSE_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": round(achieved_tf / MFMA_FP4_DENSE_TFLOPS, 4),
+            "kernel": kname_long,
+            "bound": main["bound"],
+            "achieved": main["achieved"],
+            "peak": main["peak"],
+            "unit": main["unit"],
+            "frac": main["frac"],
+            "timing": "in frame: the average of %d searches timed with HIP events on their stream, "
+                      "each after both transforms and before the agree, as in a match" % reps,
+            "back_to_back": {"ms_per_launch": round(t_b2b * 1e3, 4),
+                             "frac": round(main["frac"] * t_search / t_b2b, 4)},
+            "reverse_col1_kept": kept,
             "traffic": traffic["bytes"],
             "traffic_source": traffic.get("source") or traffic.get("why"),
             "algorithmic_bytes": search_bytes,
@@ -831,6 +939,10 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
                 "flops": used_flops,
                 "frac": round(used_flops / t_search / 1e12 / MFMA_FP4_DENSE_TFLOPS, 4),
             },
+            "fp4_view" if pk else "key_reduction_view": dict(
+                fp4 if pk else kview,
+                what="dense FP4 MFMA peak, 2 x K FLOPs per pair" if pk else
+                     "issue bound of the VALU key reduction, see valu_view"),
             "pairs_per_launch": evaluated,
             "ms_per_launch": round(t_search * 1e3, 4),
             "peak_model": "dense FP4 MFMA peak (MI355X_MICROARCH.md); algorithmic FLOPs = 2 x K "
@@ -843,8 +955,9 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
                 "source": "profiles/mfma_rates_r01.jsonl (tools/mfma_rate.hip, 4 waves/SIMD)",
             },
             "valu_view": {
-                "what": "the VALU key reduction (v_min3 + v_xor per pair) that bounds the "
-                        "kernel; issue bound at the measured rates, see DESIGN.md s5",
+                "what": ("the VALU key reduction (packed f16 trees, pk_key_pair_peak)" if pk else
+                         "the VALU key reduction (v_min3 + v_xor per pair) that co-bounds the "
+                         "kernel") + "; issue bound at the measured rates, see DESIGN.md s5",
                 "achieved_Gpairs": round(evaluated / t_search / 1e9, 1),
                 "peak_Gpairs": round(kpeak, 1),
                 "frac": round(evaluated / t_search / 1e9 / kpeak, 4),

@@ -19,6 +19,7 @@
 #include "engine.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <string>
@@ -79,16 +80,36 @@ void band_stage_offsets(size_t& off, int rows, int cols, size_t dsz, size_t csz,
 }
 
 // Let `peer` read and write memory of `owner`'s default stream-ordered pool (hipMallocAsync,
-// which peer access does not cover).
-int share_pool(int owner, int peer) {
+// which peer access does not cover). No error string: a refusal is not an error of the match.
+bool share_pool(int owner, int peer) {
     hipMemPool_t pool = nullptr;
-    int rc = check_hip(hipDeviceGetDefaultMemPool(&pool, owner), "hipDeviceGetDefaultMemPool");
-    if (rc) return rc;
+    if (hipDeviceGetDefaultMemPool(&pool, owner) != hipSuccess) return false;
     hipMemAccessDesc d{};
     d.location.type = hipMemLocationTypeDevice;
     d.location.id = peer;
     d.flags = hipMemAccessFlagsProtReadWrite;
-    return check_hip(hipMemPoolSetAccess(pool, &d, 1), "hipMemPoolSetAccess");
+    return hipMemPoolSetAccess(pool, &d, 1) == hipSuccess;
+}
+
+// Direct xGMI peer DMA from `dev` (the current device) into `root`'s maps, all or nothing
+// (ADVICE r04): peer access in both directions AND each device's pool open to the other. A
+// partial grant -- peer access on, a pool closed -- would let the copy engine DMA into memory
+// it has no mapping for, so then the peer access this call enabled is switched off again and
+// the caller copies through pinned host memory instead. Nothing here sets the error string.
+bool enable_peer_path(int dev, int root) {
+    int fwd = 0, back = 0;
+    bool ok = hipDeviceCanAccessPeer(&fwd, dev, root) == hipSuccess && fwd &&
+              hipDeviceCanAccessPeer(&back, root, dev) == hipSuccess && back;
+    bool enabled_here = false;
+    if (ok) {
+        const hipError_t pe = hipDeviceEnablePeerAccess(root, 0);
+        enabled_here = pe == hipSuccess;
+        ok = pe == hipSuccess || pe == hipErrorPeerAccessAlreadyEnabled;
+    }
+    ok = ok && share_pool(dev, root) && share_pool(root, dev);
+    if (!ok && enabled_here) (void)hipDeviceDisablePeerAccess(root);
+    (void)hipGetLastError();  // clear a sticky refusal / "already enabled"
+    return ok;
 }
 
 float nxc_threshold(const BicosConfig& cfg) {
@@ -205,34 +226,41 @@ extern "C" int bicos_match_bands_device(const int* devices, int ndev, const void
         // stage layout per device: the same offsets the enqueue loop below takes
         // (band_stage_offsets), so the reservation covers the last byte written
         std::map<int, size_t> stage_need;
+        std::map<int, int> copies;  // bands per device (host-staged copies: one event each)
         for (int b = 1; b < ndev; ++b) {
             size_t sd = 0, sc = 0;
             band_stage_offsets(stage_need[devices[b]], band_rows[b], cols, dsz, corrmap ? csz : 0,
                                &sd, &sc);
+            ++copies[devices[b]];
         }
+        // per device: true = direct peer DMA into the root's maps (or a device-local copy on
+        // the root itself), false = through pinned host memory (enable_peer_path refused).
+        // UNVERIFIED on distinct GPUs until a multi-GPU box runs tests/test_multi_gpu.py.
+        // BICOS_GATHER_HOST=1 takes the host-staged path everywhere (read per call: the
+        // one-GPU test of that path, tests/test_multi_gpu.py)
+        const bool force_host = std::getenv("BICOS_GATHER_HOST") != nullptr;
+        std::map<int, bool> direct;
         for (auto& kv : stage_need) {
             bicos_engine* e = engines[kv.first];
             rc = reserve(e->stage, e->stage_bytes, kv.second, e->device, e->own_stream, e->ws_ready);
             if (!rc) rc = check_hip(hipSetDevice(e->device), "hipSetDevice");
             if (!rc) rc = check_hip(hipStreamWaitEvent(e->own_stream, e->ws_ready, 0), "hipStreamWaitEvent");
-            if (!rc && e->device != root) {
-                // direct xGMI peer DMA into the root's maps where the link allows it, in both
-                // directions. Every step here is an optimisation: hipMemcpyPeerAsync copies
-                // between any two devices without peer access (staged by the runtime), so a
-                // refusal only costs speed and is not an error of the match. UNVERIFIED on
-                // distinct GPUs until a multi-GPU box runs tests/test_multi_gpu.py.
-                int fwd = 0, back = 0;
-                if (hipDeviceCanAccessPeer(&fwd, e->device, root) == hipSuccess && fwd &&
-                    hipDeviceCanAccessPeer(&back, root, e->device) == hipSuccess && back) {
-                    const hipError_t pe = hipDeviceEnablePeerAccess(root, 0);
-                    (void)hipGetLastError();  // clear a sticky "already enabled" / refusal
-                    // peer access does not cover stream-ordered pool memory: the stage comes
-                    // from this device's default pool (hipMallocAsync) and the root's maps may
-                    // too, so grant each device access to the other's pool explicitly
-                    if ((pe == hipSuccess || pe == hipErrorPeerAccessAlreadyEnabled) &&
-                        share_pool(e->device, root) == 0)
-                        (void)share_pool(root, e->device);
-                    (void)hipGetLastError();
+            direct[e->device] = !force_host && (e->device == root || (!rc && enable_peer_path(e->device, root)));
+            if (!rc && !direct[e->device]) {
+                // the host-staged gather: the stage layout mirrored in this engine's pinned
+                // buffer, one event per band for the root's stream to wait on
+                if (e->pinned_bytes < kv.second) {
+                    if (e->pinned) (void)hipHostFree(e->pinned);
+                    e->pinned = nullptr;
+                    e->pinned_bytes = 0;
+                    rc = check_hip(hipHostMalloc(&e->pinned, kv.second, hipHostMallocDefault),
+                                   "hipHostMalloc(gather staging)");
+                    if (!rc) e->pinned_bytes = kv.second;
+                }
+                while (!rc && (int)e->events.size() < copies[e->device]) {
+                    hipEvent_t ev;
+                    rc = check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+                    if (!rc) e->events.push_back(ev);
                 }
             }
             if (rc) {
@@ -240,6 +268,8 @@ extern "C" int bicos_match_bands_device(const int* devices, int ndev, const void
                 return rc;
             }
         }
+        bicos_engine* re = engines[root];
+        std::map<int, int> ev_used;
         // enqueue every band (asynchronous per device), then drain
         std::map<int, size_t> used;
         long r0 = 0;
@@ -267,14 +297,29 @@ extern "C" int bicos_match_bands_device(const int* devices, int ndev, const void
             char* sc = corrmap ? (char*)e->stage + oc : nullptr;
             rc = match_device(e, stack0[b], stack1[b], n, br, cols, row_pitch[b], plane_pitch[b],
                               depth, *cfg, has_nxcorr != 0, thr, sd, sc, e->own_stream);
-            if (!rc)
-                rc = check_hip(hipMemcpyPeerAsync(dst_d, root, sd, e->device, (size_t)br * cols * dsz,
-                                                  e->own_stream),
-                               "gather (peer copy)");
+            const size_t bd = (size_t)br * cols * dsz, bc = (size_t)br * cols * csz;
+            if (direct[e->device]) {
+                if (!rc)
+                    rc = check_hip(hipMemcpyPeerAsync(dst_d, root, sd, e->device, bd, e->own_stream),
+                                   "gather (peer copy)");
+                if (!rc && corrmap)
+                    rc = check_hip(hipMemcpyPeerAsync(dst_c, root, sc, e->device, bc, e->own_stream),
+                                   "gather (peer copy)");
+                continue;
+            }
+            // host-staged: down on the band's stream, up on the root's once that is done
+            char* hd = (char*)e->pinned + od;
+            char* hc = corrmap ? (char*)e->pinned + oc : nullptr;
+            hipEvent_t ev = e->events[ev_used[e->device]++];
+            if (!rc) rc = check_hip(hipMemcpyAsync(hd, sd, bd, hipMemcpyDeviceToHost, e->own_stream), "gather (download)");
             if (!rc && corrmap)
-                rc = check_hip(hipMemcpyPeerAsync(dst_c, root, sc, e->device, (size_t)br * cols * csz,
-                                                  e->own_stream),
-                               "gather (peer copy)");
+                rc = check_hip(hipMemcpyAsync(hc, sc, bc, hipMemcpyDeviceToHost, e->own_stream), "gather (download)");
+            if (!rc) rc = check_hip(hipEventRecord(ev, e->own_stream), "hipEventRecord");
+            if (!rc) rc = check_hip(hipSetDevice(root), "hipSetDevice");
+            if (!rc) rc = check_hip(hipStreamWaitEvent(re->own_stream, ev, 0), "hipStreamWaitEvent");
+            if (!rc) rc = check_hip(hipMemcpyAsync(dst_d, hd, bd, hipMemcpyHostToDevice, re->own_stream), "gather (upload)");
+            if (!rc && corrmap)
+                rc = check_hip(hipMemcpyAsync(dst_c, hc, bc, hipMemcpyHostToDevice, re->own_stream), "gather (upload)");
         }
         // drain every engine's stream whatever happened; the stage is reused next call
         for (auto& kv : engines) {

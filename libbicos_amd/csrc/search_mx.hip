@@ -204,9 +204,17 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 //
 // A workgroup scans one row for the col0 range [c0_base + tile * waves * T * 32, + waves * T *
 // 32), c0_base = a.tail_col0 for the tail launch (launch_mx), else 0.
-template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL>
+//
+// LIST: the col0 of row r are the lcount[r] compacted entries list[r][i] (Consistency's
+// reverse search over the col1 its forward search kept, see make_reverse_list in engine.cpp);
+// the index ranges above run over i, workgroups past the row's count exit at once, and the
+// block order starts REV_AHEAD columns above the wave's highest entry (a reverse match lies
+// at col0 = col1 + d, d >= 0 in a rectified pair).
+constexpr int REV_AHEAD = 64;
+template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIST>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KSU >= 4 ? 3 : 4)))
 void search_mx_kernel(SearchArgs a) {
+    static_assert(!(TAIL && LIST), "compacted searches have no tail launch");
     constexpr bool FK = KEYS == 3;
     static_assert(!FK || !NODUPES, "FK keys: first minimum only");
     constexpr bool XK = KEYS == 1 || KEYS == 2;
@@ -241,6 +249,15 @@ void search_mx_kernel(SearchArgs a) {
     const int chunk = a.chunk;
     const int waves = blockDim.x >> 6;
     const int c0_wave = c0_base + (tile * waves + wave) * (T * 32);
+    // col0 entries of this row (LIST: the compacted count; workgroup-uniform)
+    const int lcols = LIST ? __builtin_amdgcn_readfirstlane(a.lcount[row]) : cols;
+    const int16_t* __restrict__ lrow = LIST ? a.list + (size_t)row * a.list_pitch : nullptr;
+    if (LIST && tile * waves * T * 32 >= lcols) return;  // the whole workgroup: no barrier yet
+    // LIST: the column of entry i (ascending in i); the block order's start for entries < e
+    auto lcol = [&](int i) { return LIST ? (int)lrow[i] : i; };
+    auto start_col = [&](int e) {
+        return LIST ? min(cols - 1, (int)lrow[min(e, lcols) - 1] + REV_AHEAD) : min(cols - 1, e - 1);
+    };
 
     const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
     const uint32_t* __restrict__ row1 = a.desc1 + (size_t)row * a.desc_pitch;
@@ -250,11 +267,12 @@ void search_mx_kernel(SearchArgs a) {
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const int c0 = c0_wave + 32 * t + j;
+        const int cl = c0 < lcols ? lcol(c0) : 0;
 #pragma unroll
         for (int s = 0; s < KS; ++s) {
             const int w = 2 * s + h;
             uint32_t x = 0;
-            if (c0 < cols && w < WORDS) x = row0[(size_t)c0 * WORDS + w];
+            if (c0 < lcols && w < WORDS) x = row0[(size_t)cl * WORDS + w];
             if (WORDS == 8 && KS == 4 && w == 7) x &= 0x7FFFFFFFu;  // bit 255 masked (see below)
             bf[t][s] = expand_bits(x, LUT_B);
         }
@@ -393,11 +411,11 @@ void search_mx_kernel(SearchArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) cx[r] = XK_BIAS + (float)(K0 + rrow(r)) * XK_EPS;
 
-    const bool idle = c0_wave >= cols;  // wave-uniform; still joins the barriers
+    const bool idle = c0_wave >= lcols;  // wave-uniform; still joins the barriers
     const int nchunks = (cols + chunk - 1) / chunk;
     // FREE: chunks downwards from the one holding the workgroup's highest col0
     int cstart = 0;
-    if constexpr (FREE) cstart = min(cols - 1, c0_base + (tile + 1) * waves * T * 32 - 1) / chunk;
+    if constexpr (FREE) cstart = start_col(c0_base + (tile + 1) * waves * T * 32) / chunk;
     for (int k = 0; k < nchunks; ++k) {
         int ci = FREE ? cstart - k : k;
         if (ci < 0) ci += nchunks;
@@ -519,7 +537,7 @@ void search_mx_kernel(SearchArgs a) {
         if constexpr (FREE) {
             if (partial) partial_block(cc);
             // full blocks downwards from the one holding the wave's highest col0 (clamped)
-            const int sb = max(0, min(nfull - 1, (c0_wave + 32 * T - 1 - base) / 32));
+            const int sb = max(0, min(nfull - 1, (start_col(c0_wave + 32 * T) - base) / 32));
 #if !defined(BICOS_MX_DIAG) || BICOS_MX_DIAG >= 3
             if constexpr (PIPE) {
                 // software pipeline over the blocks (one tile pair per wave): the products of
@@ -636,8 +654,9 @@ void search_mx_kernel(SearchArgs a) {
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         if ((t & 1) != h) continue;  // half 0 writes even tiles, half 1 odd tiles
-        const int c0 = c0_wave + 32 * t + jo;
-        if (c0 >= cols) continue;
+        const int c0i = c0_wave + 32 * t + jo;
+        if (c0i >= lcols) continue;
+        const int c0 = lcol(c0i);
         const int best = best_of(t);
         const bool ok = unique_of(t, best);
         int16_t v;
@@ -749,11 +768,13 @@ __device__ __forceinline__ v16f mfma_pk(v4i a, v4i b, v16f c, int sb) {
 }
 
 // T wide tiles (64 col0 each) per wave; T = 1 or an even count (tiles reduced in pairs);
-// TAIL: the col0 range starts at a.tail_col0 (the tail launch, as search_mx_kernel's)
-template <int WORDS, int T, bool TAIL>
+// TAIL: the col0 range starts at a.tail_col0 (the tail launch, as search_mx_kernel's);
+// LIST: compacted col0 entries (as search_mx_kernel's)
+template <int WORDS, int T, bool TAIL, bool LIST>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void search_pk_kernel(SearchArgs a) {
     static_assert(T == 1 || T % 2 == 0, "wide tiles: 1 or pairs");
+    static_assert(!(TAIL && LIST), "compacted searches have no tail launch");
     constexpr int NP = T == 1 ? 1 : T / 2;
     extern __shared__ __attribute__((aligned(16))) v4i lds_mx[];  // [WORDS][chunk]
 
@@ -774,6 +795,13 @@ void search_pk_kernel(SearchArgs a) {
     const int waves = blockDim.x >> 6;
     const int c0_base = TAIL ? a.tail_col0 : 0;
     const int c0_wave = c0_base + (tile * waves + wave) * (T * 64);
+    const int lcols = LIST ? __builtin_amdgcn_readfirstlane(a.lcount[row]) : cols;
+    const int16_t* __restrict__ lrow = LIST ? a.list + (size_t)row * a.list_pitch : nullptr;
+    if (LIST && tile * waves * T * 64 >= lcols) return;  // the whole workgroup: no barrier yet
+    auto lcol = [&](int i) { return LIST ? (int)lrow[i] : i; };
+    auto start_col = [&](int e) {
+        return LIST ? min(cols - 1, (int)lrow[min(e, lcols) - 1] + REV_AHEAD) : min(cols - 1, e - 1);
+    };
 
     const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
     const uint32_t* __restrict__ row1 = a.desc1 + (size_t)row * a.desc_pitch;
@@ -784,9 +812,10 @@ void search_pk_kernel(SearchArgs a) {
 #pragma unroll
     for (int t = 0; t < T; ++t) {
         const int c0 = c0_wave + 64 * t + lane;
+        const int cl = c0 < lcols ? lcol(c0) : 0;
 #pragma unroll
         for (int w = 0; w < WORDS; ++w) {
-            const uint32_t x = c0 < cols ? row0[(size_t)c0 * WORDS + w] : 0u;
+            const uint32_t x = c0 < lcols ? row0[(size_t)cl * WORDS + w] : 0u;
             bf[t][w] = expand_bits(x, LUT_PB);
         }
     }
@@ -857,12 +886,12 @@ void search_pk_kernel(SearchArgs a) {
         }
     };
 
-    const bool idle = c0_wave >= cols;  // wave-uniform; still joins the barriers
+    const bool idle = c0_wave >= lcols;  // wave-uniform; still joins the barriers
     const int nchunks = (cols + chunk - 1) / chunk;
     // chunks downwards from the one holding the workgroup's highest col0, blocks downwards
     // from the wave's highest col0 (stereo matches lie at col1 <= col0 within a few blocks,
     // so the running minimum is found early and later blocks rarely take the branch)
-    const int cstart = min(cols - 1, c0_base + (tile + 1) * waves * T * 64 - 1) / chunk;
+    const int cstart = start_col(c0_base + (tile + 1) * waves * T * 64) / chunk;
     for (int k = 0; k < nchunks; ++k) {
         int ci = cstart - k;
         if (ci < 0) ci += nchunks;
@@ -913,7 +942,7 @@ void search_pk_kernel(SearchArgs a) {
             }
         };
         if ((ncols & 31) != 0) block(nfull, true);
-        const int sb0 = max(0, min(nfull - 1, (c0_wave + 64 * T - 1 - base) / 32));
+        const int sb0 = max(0, min(nfull - 1, (start_col(c0_wave + 64 * T) - base) / 32));
         for (int i = 0; i < nfull; ++i) {
             int b = sb0 - i;
             if (b < 0) b += nfull;
@@ -931,8 +960,9 @@ void search_pk_kernel(SearchArgs a) {
         const int t = T == 1 ? 0 : 2 * p + h;
 #pragma unroll
         for (int f = 0; f < 2; ++f) {  // f = 0: high field (col0 P), 1: low field (Q = P + 32)
-            const int c0 = c0_wave + 64 * t + 32 * f + jo;
-            if (c0 >= cols) continue;
+            const int c0i = c0_wave + 64 * t + 32 * f + jo;
+            if (c0i >= lcols) continue;
+            const int c0 = lcol(c0i);
             const int sh = f ? 0 : 16;
             const int best = (int)((C[p] >> sh) & 0xFFFFu);
             const bool ok = ((M[p] >> sh) & 0xFFFFu) != 0u;
@@ -946,10 +976,10 @@ void search_pk_kernel(SearchArgs a) {
     }
 }
 
-template <int WORDS, int T, bool TAIL>
+template <int WORDS, int T, bool TAIL, bool LIST = false>
 hipError_t launch_pk_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st) {
     const size_t lds = (size_t)WORDS * a.chunk * 16;
-    const auto kern = search_pk_kernel<WORDS, T, TAIL>;
+    const auto kern = search_pk_kernel<WORDS, T, TAIL, LIST>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -979,6 +1009,11 @@ inline void tail_shape(SearchArgs& t, int& waves, int cols_per_wave) {
 // over [tail_col0, cols) when the geometry asked for one (see launch_mx_tt)
 template <int WORDS, int T>
 hipError_t launch_pk(const SearchArgs& a, int waves, hipStream_t st) {
+    if (a.list) {  // compacted col0: workgroups for the whole width, those past the count exit
+        SearchArgs b = a;
+        b.tiles_per_row = (int)((a.cols + 64L * waves * T - 1) / (64L * waves * T));
+        return launch_pk_grid<WORDS, T, false, true>(b, waves, a.rows * b.tiles_per_row, st);
+    }
     hipError_t e = launch_pk_grid<WORDS, T, false>(a, waves, a.rows * a.tiles_per_row, st);
     if constexpr (T > 1) {
         if (e == hipSuccess && a.tail_col0 < a.cols) {
@@ -1002,11 +1037,11 @@ hipError_t launch_pk_w(const SearchArgs& a, const MxGeometry& g, hipStream_t st)
     return hipErrorInvalidValue;
 }
 
-template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL>
+template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIST = false>
 hipError_t launch_mx_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st) {
     constexpr int WL = 2 * KSU;
     const size_t lds = (size_t)WL * a.chunk * 16;
-    const auto kern = search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, TAIL>;
+    const auto kern = search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, TAIL, LIST>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1042,10 +1077,10 @@ hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     // (tail tiles: 1 or 2, and fewer than the main workgroups'; KEYS 2 only -- the any-order
     // NoDuplicates search, whose block order starts at each wave's own col0)
     if constexpr (KEYS == 2 && T >= 2) {
-        if (a.tail_T == 1 && a.tail_col0 < a.cols) return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 1>(a, waves, st);
+        if (!a.list && a.tail_T == 1 && a.tail_col0 < a.cols) return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 1>(a, waves, st);
     }
     if constexpr (KEYS == 2 && T >= 4) {
-        if (a.tail_T == 2 && a.tail_col0 < a.cols) return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 2>(a, waves, st);
+        if (!a.list && a.tail_T == 2 && a.tail_col0 < a.cols) return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 2>(a, waves, st);
     }
     // no tail workgroups for these keys / tile counts: the main workgroups cover every col0
     SearchArgs b = a;
@@ -1053,6 +1088,8 @@ hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     b.tiles_per_row = (int)((a.cols + per_wg - 1) / per_wg);
     b.tail_T = 0;
     b.tail_col0 = a.cols;
+    if (a.list)  // compacted col0: the workgroups past a row's count exit at once
+        return launch_mx_grid<WORDS, KSU, NODUPES, T, KEYS, false, true>(b, waves, a.rows * b.tiles_per_row, st);
     return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 0>(b, waves, st);
 }
 
@@ -1167,7 +1204,9 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     // at 128 bits it measured slower, 0.336 vs 0.311 ms at cfg2, profiles/pk_keys_r03.jsonl),
     // or wherever variant 68 asks for it. Same workgroup shape, a wide tile = two 32-col0
     // tiles; the LDS stage holds one expanded word per descriptor word
-    g.pk = (keys == 4 || (keys == 0 && words <= 2)) && bits > 0 && bits <= PK_MAX_BITS && bits <= 32 * words &&
+    // (32/64-bit words need no used-bits hint: a distance is at most 64 <= PK_MAX_BITS)
+    g.pk = (keys == 4 || (keys == 0 && words <= 2)) &&
+           (words <= 2 || (bits > 0 && bits <= PK_MAX_BITS)) && bits <= 32 * words &&
            (words == 1 || words == 2 || words == 4) && cols <= PK_MAX_COLS;
     g.pk_T = g.T >= 2 ? g.T / 2 : 1;
     if (words == 4 && g.pk_T > 2) g.pk_T = 2;  // (4 wide tiles' B fragments do not fit)

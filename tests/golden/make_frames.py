@@ -77,18 +77,21 @@ FRAMES = {
 #   lowtex      LIMITED n = 33 descriptors of a weakly textured scene (synthetic
 #               low_texture_stack: 8 grey levels in 4-column runs + independent noise, right
 #               view moved 5 columns) -- duplicate and tied minima decide ~30 % of pixels
-SEARCH_SHAPE = (2200, 3300, 4)
+# Round 5: random_u32 / random_u64, the reference bench's 32- and 64-bit descriptor points
+# (bench/cuda.cu:353-366; the packed-key search at size), every descriptor bit random.
+SEARCH_SHAPE = (2200, 3300)
 SEARCH_FLAGS = {"nodupes": (1, -1), "cons": (2, 3), "both": (3, 3)}
-SEARCH_INPUTS = ("random", "periodic64", "lowtex")
+SEARCH_INPUTS = {"random": 4, "periodic64": 4, "lowtex": 4, "random_u32": 1, "random_u64": 2}
 SEARCH_FRAMES = {"search_%s_%s" % (i, f): (i, f) for i in SEARCH_INPUTS for f in SEARCH_FLAGS}
 
 
 def search_inputs(kind, O=None, row_begin=0, row_end=None):
-    """(left, right) descriptor words [rows, W, 4] uint32 of rows [row_begin, row_end) of an
-    input, and its used-bits hint."""
-    H, W, words = SEARCH_SHAPE
+    """(left, right) descriptor words [rows, W, words] uint32 of rows [row_begin, row_end) of
+    an input, and its used-bits hint."""
+    H, W = SEARCH_SHAPE
+    words = SEARCH_INPUTS[kind]
     rows = dict(row_begin=row_begin, row_end=row_end)
-    if kind == "random":
+    if kind in ("random", "random_u32", "random_u64"):
         return (random_descriptors(H, W, words, SEED, **rows),
                 random_descriptors(H, W, words, SEED ^ 0xA5A5A5A5, **rows), 0)
     if kind == "periodic64":
@@ -147,7 +150,8 @@ def frame_record(n, H, W, cfg, L, R, d, c, maxval=None):
 def search_record(name, O):
     kind, fl = SEARCH_FRAMES[name]
     flags, lr = SEARCH_FLAGS[fl]
-    H, W, words = SEARCH_SHAPE
+    H, W = SEARCH_SHAPE
+    words = SEARCH_INPUTS[kind]
     d0, d1, bits = search_inputs(kind, O)
     d = O.search(d0, d1, flags, lr, variant="v3")
     # the numpy restatement agrees on two rows (tests/test_oracle.py cross-checks the rest)

@@ -64,7 +64,8 @@ def _frames():
 
 
 def test_frames_cover_every_config():
-    from tests.golden.make_frames import FRAMES, SEARCH_FLAGS, SEARCH_FRAMES, SEARCH_SHAPE
+    from tests.golden.make_frames import (FRAMES, SEARCH_FLAGS, SEARCH_FRAMES, SEARCH_INPUTS,
+                                          SEARCH_SHAPE)
     db = _frames()
     assert sorted(db) == sorted(list(FRAMES) + list(SEARCH_FRAMES))
     for name, spec in FRAMES.items():
@@ -76,7 +77,7 @@ def test_frames_cover_every_config():
         assert len(r["disparity_bands"]) == -(-H // r["band_rows"])
     for name, (kind, fl) in SEARCH_FRAMES.items():
         r = db[name]
-        assert (r["H"], r["W"], r["words"]) == SEARCH_SHAPE
+        assert (r["H"], r["W"], r["words"]) == SEARCH_SHAPE + (SEARCH_INPUTS[kind],)
         assert (r["input"], r["flags"], r["max_lr_diff"]) == (kind,) + SEARCH_FLAGS[fl]
         assert len(r["disparity_bands"]) == -(-r["H"] // r["band_rows"])
 
@@ -96,7 +97,7 @@ def test_oracle_reproduces_frame_band0(oracle, name):
     assert band_hashes(c, rows)[0] == rec["corrmap_bands"][0]
 
 
-@pytest.mark.parametrize("kind", ["random", "periodic64", "lowtex"])
+@pytest.mark.parametrize("kind", ["random", "periodic64", "lowtex", "random_u32", "random_u64"])
 def test_oracle_reproduces_search_band0(oracle, kind):
     from tests.golden.make_frames import SEARCH_FLAGS, band_hashes, search_inputs
     db = _frames()

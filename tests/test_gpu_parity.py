@@ -253,6 +253,43 @@ def test_agree_window_spans(gpu, oracle, n):
         same(host(corr), rc)
 
 
+# The whole-right-row agree (kernels.hip agree_row_kernel, BICOS_AGREE_ROW=1 -- read per
+# call): the disparity patterns above (negative disparities, matches off the row, NaN
+# correlations), widths that are not a multiple of 16 or of a workgroup, u16 stacks, n past
+# its bucket, and whole frames against the oracle's fixtures
+@pytest.mark.parametrize("n,dt,W", [(2, np.uint8, 1024), (8, np.uint8, 1000), (33, np.uint8, 2048),
+                                    (33, np.uint8, 1030), (17, np.uint16, 777), (40, np.uint8, 2048),
+                                    (65, np.uint8, 600), (12, np.uint16, 3000)])
+@pytest.mark.parametrize("minvar", [None, 2.0])
+def test_agree_row_kernel(gpu, oracle, monkeypatch, n, dt, W, minvar):
+    monkeypatch.setenv("BICOS_AGREE_ROW", "1")
+    H = 8
+    L, R = stereo_stack(n, H, W, dt, dmin=3, drange=40, seed=n + 5)
+    rng = np.random.default_rng(n + W)
+    raw = np.empty((H, W), np.int16)
+    raw[0] = 17
+    raw[1] = 20 + rng.integers(-1, 2, size=W)
+    raw[2] = np.where(np.arange(W) % 64 < 32, 5, 250)
+    raw[3] = rng.integers(-40, W + 40, size=W)              # anything, incl. off-row matches
+    raw[4] = 12
+    raw[4, ::7] = -32768
+    raw[5] = np.arange(W) % 9 - 4                            # negative disparities
+    raw[6] = W - 1                                           # only the last column matches
+    raw[7] = -32768
+    R[:, 0, 40:48] = 9                                       # flat right pixels: NaN correlations
+    mv = None if minvar is None else np.float32(minvar) * np.float32(n)
+    rd, rc = oracle.agree(raw, L, R, 0.5, mv)
+    out, corr = gpu.agree(dev(raw), dev(L), dev(R), 0.5, None if mv is None else float(mv))
+    same(host(out), rd.astype(np.float32))
+    same(host(corr), rc)
+
+
+@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "cfg2_u16", "full_n8", "cfg5"])
+def test_full_frame_agree_row(gpu, oracle, monkeypatch, name):
+    monkeypatch.setenv("BICOS_AGREE_ROW", "1")
+    _check_frame(gpu, oracle, name)
+
+
 # n covers exact buckets and padded ones (2, 12, 25, 45, 60: slots n..MAXN-1 are exact
 # no-ops) in both loop structures (pipelined MAXN <= 40, top-of-step above); steps cover
 # 41/20/8 x values, 3 and a single x (step > 2)
@@ -491,8 +528,11 @@ def test_full_frame_modes(gpu, oracle, name):
 # The search's hard paths at size: the int16 result of bicos_search_device on 128-bit
 # descriptors at 3300x2200 (the reference kernel-bench shape) -- random, periodic-64 (every
 # minimum duplicated) and low-texture (ties decide ~30 % of pixels) -- through NODUPES,
-# CONSISTENCY and NODUPES|CONSISTENCY (max_lr_diff 3), every pixel against the oracle's hash
-_SEARCH_NAMES = ["search_%s_%s" % (i, f) for i in ("random", "periodic64", "lowtex")
+# CONSISTENCY and NODUPES|CONSISTENCY (max_lr_diff 3), every pixel against the oracle's hash;
+# round 5: random 32- and 64-bit descriptors (the reference bench's other widths, the
+# packed-key search at size)
+_SEARCH_NAMES = ["search_%s_%s" % (i, f)
+                 for i in ("random", "periodic64", "lowtex", "random_u32", "random_u64")
                  for f in ("nodupes", "cons", "both")]
 _SEARCH_IN = {}
 
@@ -508,7 +548,7 @@ def test_full_frame_search_inputs(gpu, oracle, name):
         d0, d1, bits = search_inputs(rec["input"], oracle)
         assert [sha(d0), sha(d1)] == rec["inputs_sha256"], "descriptor generator changed"
         pitch = gpu._L.bicos_desc_pitch(W, words)
-        assert pitch == W * words  # 3300 x 4 words: rows need no padding
+        assert pitch == W * words  # 3300 x 1/2/4 words: rows need no padding
         _SEARCH_IN[rec["input"]] = (
             d0, d1, torch.from_numpy(d0.view(np.int32).reshape(H, pitch)).cuda(),
             torch.from_numpy(d1.view(np.int32).reshape(H, pitch)).cuda(), bits)

@@ -185,3 +185,25 @@ def test_bands_device_one_row_bands_of_narrow_frames(gpu, W, kw):
     same(host(dm), host(d1))
     if c1 is not None:
         same(host(cm), host(c1))
+
+
+@pytest.mark.parametrize("kw,k", [({}, 4), ({"nxcorr_threshold": None}, 3),
+                                  ({"subpixel_step": 0.25, "precision": 1}, 3)])
+def test_bands_device_host_staged_gather(gpu, monkeypatch, kw, k):
+    """The gather's fallback when direct peer DMA is refused (multi.cpp enable_peer_path:
+    all or nothing): every band's maps go down to the engine's pinned buffer on
+    the band's stream and up into the root's maps on the root's stream behind an event.
+    BICOS_GATHER_HOST=1 forces that path, so the one-GPU box runs it too."""
+    from libbicos_amd.device import MatchConfig, match_bands
+    L, R = stereo_stack(33, 45, 384)
+    s0, s1 = dev(L), dev(R)
+    cfg = MatchConfig(**kw)
+    d1, c1 = gpu.match(s0, s1, cfg)
+    b = _bands(45, k)
+    monkeypatch.setenv("BICOS_GATHER_HOST", "1")
+    for _ in range(2):  # the second call reuses the pinned buffer and its events
+        dm, cm = match_bands(_place([s0[:, r0:r1] for r0, r1 in b]),
+                             _place([s1[:, r0:r1] for r0, r1 in b]), cfg)
+        same(host(dm), host(d1))
+        if c1 is not None:
+            same(host(cm), host(c1))

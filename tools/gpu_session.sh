@@ -173,6 +173,27 @@ for step in "$@"; do
             run tunepipe 600 python tools/frame_pipe_bench.py --ns 1 --streams 1,2,3 --rounds 2 --reps 40 --tunes ${TUNES:-0:0:0:0,64:4:4:48,64:4:4:40,64:4:6:64,64:2:8:64,64:4:8:64} ;;
         refk) run refk 600 python tools/ref_kernel_bench.py --out gpurun_out/ref_kernel_bench.jsonl ;;
         randsearch) run randsearch 600 python tools/random_search_bench.py --out gpurun_out/random_search.jsonl ;;
+        rootload)  # rank 0 of an N = 8 run on one GPU: band-of-8 with 3 frames in flight, without / with the gather ingress (CU copy kernel, DMA)
+            for k in 1 2; do for c in ${SCS:-cfg2 cfg5}; do
+                for m in none kernel dma; do
+                    run rl_${c}_${m}$k 300 python bench.py --config $c --band-of ${RLN:-8} --inflight 3 --steps 400 --warmup 10 --no-cpu-baseline --no-host-path --kernel-reps 0 $([ $m = none ] || echo --root-load $m)
+                done
+            done; done ;;
+        agreeab)  # whole-right-row agree (BICOS_AGREE_ROW=1) vs the LDS-tile agree, whole bench lines, interleaved twice
+            for k in 1 2; do for c in ${SCS:-cfg2 cfg4 cfg5}; do
+                run agree_${c}_tile$k 300 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline --no-host-path
+                BICOS_AGREE_ROW=1 run agree_${c}_row$k 300 python bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline --no-host-path
+            done; done ;;
+        agreeprof)  # kernel stats one frame at a time, both agree kernels (cfg2)
+            run agreeprof_tile 300 rocprofv3 --kernel-trace --stats -d gpurun_out/agreeprof_tile -o run --output-format csv -- python bench.py --config ${SC:-cfg2} --steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --no-host-path
+            BICOS_AGREE_ROW=1 run agreeprof_row 300 rocprofv3 --kernel-trace --stats -d gpurun_out/agreeprof_row -o run --output-format csv -- python bench.py --config ${SC:-cfg2} --steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --no-host-path ;;
+        revab)  # Consistency's reverse search over the kept col1 vs the full reverse pass (BICOS_REV_FULL=1)
+            run randsearch_kept 600 python tools/random_search_bench.py --words 1,2,4 --out gpurun_out/random_search_kept.jsonl
+            BICOS_REV_FULL=1 run randsearch_full 600 python tools/random_search_bench.py --words 1,2,4 --out gpurun_out/random_search_full.jsonl
+            for k in 1 2; do
+                run bench4_kept$k 300 python bench.py --config cfg4 --steps 20 --warmup 3 --no-cpu-baseline --no-host-path
+                BICOS_REV_FULL=1 run bench4_full$k 300 python bench.py --config cfg4 --steps 20 --warmup 3 --no-cpu-baseline --no-host-path
+            done ;;
         benchall)  # one bench line per BASELINE config + the README shape (cfg2 with host path)
             run bench_cfg2 300 python bench.py --config cfg2 --steps 20 --warmup 3
             for c in cfg3 cfg4 cfg5 readme cfg1; do
