@@ -350,12 +350,18 @@ def main():
     ap.add_argument("--band-of", type=int, default=1,
                     help="one process, band 0 of an N-way row split (no gather): the band a "
                          "rank of an N-GPU run computes, for profiling at band sizes")
-    ap.add_argument("--root-load", default=None, choices=["kernel", "dma"],
+    ap.add_argument("--root-load", default=None, choices=["kernel", "proxy", "dma"],
                     help="with --band-of N: rehearse rank 0's gather ingress on one GPU -- per "
                          "step, on a side stream, the N-1 other bands' packed maps are written "
-                         "into a root buffer, by a CU copy kernel (RCCL's receive runs on the "
-                         "root's CUs) or by the DMA engine (a pinned-host upload; PCIe-rate, so "
-                         "at most one in flight). Reports the band's rate under that load.")
+                         "into a root buffer: by a full-grid torch copy kernel (kernel), by "
+                         "--root-load-wgs long-lived copy workgroups the way RCCL receives on the "
+                         "root's CUs (proxy: tools/ingress_proxy.hip), or by the DMA engine (dma: "
+                         "a pinned-host upload, PCIe-rate, at most one in flight). Reports the "
+                         "band's rate under that load.")
+    ap.add_argument("--root-load-wgs", type=int, default=16,
+                    help="--root-load proxy: copy workgroups (RCCL channels x peers)")
+    ap.add_argument("--root-load-high-priority", action="store_true",
+                    help="--root-load: the ingress stream at high priority")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` without torchrun: start the N ranks ourselves, before
@@ -500,24 +506,45 @@ def main():
         bpp = (2 if (i16 or not has_corr) else 4) + (4 if has_corr else 0)
         ing = (args.band_of - 1) * band_height(H, args.band_of) * W * bpp
         ing = (ing + 3) // 4 * 4
+        ing = (ing + 15) // 16 * 16
         load = {"mode": args.root_load, "bytes_per_step": ing, "issued": 0, "skipped": 0,
                 "dst": torch.empty(ing // 4, dtype=torch.int32, device=dev),
-                "src": (torch.ones(ing // 4, dtype=torch.int32, device=dev)
-                        if args.root_load == "kernel" else
-                        torch.ones(ing // 4, dtype=torch.int32).pin_memory()),
-                "stream": torch.cuda.Stream(dev), "ev": torch.cuda.Event()}
+                "src": (torch.ones(ing // 4, dtype=torch.int32).pin_memory()
+                        if args.root_load == "dma" else
+                        torch.ones(ing // 4, dtype=torch.int32, device=dev)),
+                "stream": torch.cuda.Stream(dev, priority=-1 if args.root_load_high_priority else 0),
+                "ev": torch.cuda.Event(), "ring": [torch.cuda.Event() for _ in range(max(2, F))]}
+        if args.root_load == "proxy":
+            import ctypes
+            so = os.path.join(ROOT, "build", "ingress_proxy.so")
+            if not os.path.exists(so):
+                raise SystemExit("--root-load proxy needs %s (hipcc --offload-arch=gfx950 -O3 -shared "
+                                 "-fPIC tools/ingress_proxy.hip -o %s)" % (so, so))
+            load["proxy"] = ctypes.CDLL(so)
+            load["proxy"].ingress_proxy_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p,
+                                                           ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
 
-    def issue_load():
-        # one ingress per step; the DMA form (PCIe-rate) skips a step while the last is busy
-        if load["issued"] and not load["ev"].query():
+    def issue_load(k):
+        # one ingress per step. The copy-kernel forms apply the gather pipeline's back pressure
+        # (a band buffer is rewritten only after the gather that read it, max(2, F) steps
+        # back, is done: step() waits on ring[k % len]); the DMA form (PCIe-rate) skips a step
+        # while the last one is busy instead
+        if load["mode"] == "dma" and load["issued"] and not load["ev"].query():
             load["skipped"] += 1
             return
         with torch.cuda.stream(load["stream"]):
             if load["mode"] == "kernel":
                 torch.bitwise_or(load["src"], 0, out=load["dst"])  # a CU kernel: read + write
+            elif load["mode"] == "proxy":
+                rc = load["proxy"].ingress_proxy_launch(load["dst"].data_ptr(), load["src"].data_ptr(),
+                                                        load["bytes_per_step"], args.root_load_wgs,
+                                                        load["stream"].cuda_stream)
+                if rc:
+                    raise RuntimeError("ingress_proxy_launch failed: %d" % rc)
             else:
                 load["dst"].copy_(load["src"], non_blocking=True)  # hipMemcpyAsync H2D: SDMA
             load["ev"].record(load["stream"])
+            load["ring"][k % len(load["ring"])].record(load["stream"])
         load["issued"] += 1
 
     def step():
@@ -526,9 +553,13 @@ def main():
         f = k % F  # frame slot: engine + stream
         with torch.cuda.stream(streams[f]):
             if not gather:
+                timed_load = load is not None and state.get("timed")
+                ring = load["ring"] if timed_load else None
+                if timed_load and load["mode"] != "dma" and k - state["k0"] >= len(ring):
+                    torch.cuda.current_stream(dev).wait_event(ring[k % len(ring)])
                 engines[f].match(s0, s1, mcfg, out=outs[f], corrmap=corrs[f])
-                if load is not None and state.get("timed"):
-                    issue_load()
+                if timed_load:
+                    issue_load(k)
                 return
             i = k % NB
             if pending[i] is not None:
@@ -572,6 +603,7 @@ def main():
     if world > 1:
         dist.barrier()
     state["timed"] = True
+    state["k0"] = state["k"]
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -670,10 +702,15 @@ def main():
                 "mode": load["mode"], "bytes_per_step": load["bytes_per_step"],
                 "loads_issued": load["issued"], "steps_skipped": load["skipped"],
                 "ingress_GBps": round(load["bytes_per_step"] * load["issued"] / elapsed / 1e9, 1),
+                "workgroups": args.root_load_wgs if load["mode"] == "proxy" else None,
+                "high_priority_stream": bool(args.root_load_high_priority),
+                "back_pressure": load["mode"] != "dma",
                 "what": "rank 0's gather ingress of an N = %d run rehearsed on one GPU: the other "
                         "%d bands' packed maps written per step into a root buffer on a side "
                         "stream (%s)" % (args.band_of, args.band_of - 1,
-                                         "CU copy kernel" if load["mode"] == "kernel" else
+                                         "full-grid torch copy kernel" if load["mode"] == "kernel" else
+                                         "%d long-lived copy workgroups, RCCL's receive shape" %
+                                         args.root_load_wgs if load["mode"] == "proxy" else
                                          "DMA engine, pinned-host upload at PCIe rate")},
             "verify_gather": verify,
             "cpu_baseline": cpu,

@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -476,7 +477,8 @@ __global__ __launch_bounds__(1024) void reverse_list_kernel(ReverseListArgs a) {
     __syncthreads();
     const int16_t* f = a.fwd + (size_t)row * cols;
     for (int c = tid; c < cols; c += 1024) {
-        const int b = f[c];
+        // (a.all = k > 0: every k-th col1 instead, a timing diagnostic)
+        const int b = a.all ? (c % a.all == 0 ? c : -1) : f[c];
         if (b >= 0) atomicOr(&mark[b >> 5], 1u << (b & 31));
     }
     __syncthreads();
@@ -704,116 +706,6 @@ __global__ __launch_bounds__(256) void agree_lds_kernel(AgreeArgs a) {
     if (a.corrmap) ((TPrec*)a.corrmap)[o] = corr;
 }
 
-// agree with the whole right row staged in LDS: the workgroups of a row
-// (1024 columns each, on one XCD) load all n right planes of the row with coalesced dwordx4
-// loads -- independent of the disparities, so nothing waits on the raw map before the row's
-// bytes are in flight (the second workgroup of a row finds them in its XCD's L2) -- and each
-// lane reads its n samples at col - d from LDS instead of n dependent byte gathers from HBM.
-// One pixel per lane; the left samples are per-plane byte loads at col. LDS: n x
-// round_up(cols * sizeof(TIn), 16) bytes (cfg2: 67.6 KiB, two workgroups per CU). Same
-// arithmetic, contract and results as agree_lds_kernel; 4-byte aligned stacks and pitches
-// (checked on the host).
-template <typename TIn, typename TPrec, int MAXN>
-__global__ __launch_bounds__(1024) void agree_row_kernel(AgreeArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t row1[];  // [n][wpb] bytes
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    int tile, row;
-    xcd_rows(tile, row);
-    const int n = a.n;
-    const int cols = a.cols;
-    const int bs = blockDim.x;
-    const int tid = threadIdx.x;
-    const int col = tile * bs + tid;
-    const bool live = col < cols;
-    constexpr uint32_t SZ = sizeof(TIn);
-    const uint32_t rb = ((uint32_t)cols * SZ + 15u) / 16u;  // 16-byte chunks per plane row
-    const uint32_t wpb = rb * 16u;
-    const uint32_t pp = (uint32_t)a.plane_pitch;
-    const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
-    const uint32_t range = a.stack_bytes > 0xFFFFFFFCu ? 0xFFFFFFFFu : (a.stack_bytes + 3u) & ~3u;
-    const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<void*>(a.stack1), (short)0, (int)range, 0x00020000);
-    int d = live ? (int)a.raw[(size_t)row * a.raw_pitch + col] : INVALID_I16;
-    // left samples: straight-line loads (slots past n re-read plane n-1), in flight with the
-    // row loads below
-    const StackReader<TIn> rd0(a.stack0, a.stack_bytes);
-    const uint32_t c0 = live ? (uint32_t)col : 0u;
-    uint32_t l[MAXN];
-#pragma unroll
-    for (int t = 0; t < MAXN; ++t) l[t] = rd0(c0, rowoff + (uint32_t)min(t, n - 1) * pp);
-    // the right row: n planes x rb chunks. Thread tid takes chunk i = tid % 2^lg of plane
-    // tid / 2^lg (2^lg >= rb, a power of two; checked on the host: 2^lg <= blockDim) of each
-    // pass of ppp = blockDim / 2^lg planes, RB passes of dwordx4 loads in flight per batch
-    constexpr int RB = 4;
-    const uint32_t lg = rb > 1 ? 32u - (uint32_t)__builtin_clz(rb - 1u) : 0u;
-    const uint32_t ppp = (uint32_t)bs >> lg;
-    const uint32_t i = (uint32_t)tid & ((1u << lg) - 1u);
-    const uint32_t p0 = (uint32_t)tid >> lg;
-    const bool chunk_live = i < rb && p0 < ppp;
-    for (uint32_t base = 0; base < (uint32_t)n; base += RB * ppp) {
-        v4u buf[RB];
-#pragma unroll
-        for (int k = 0; k < RB; ++k) {
-            const uint32_t p = base + p0 + (uint32_t)k * ppp;
-            buf[k] = chunk_live && p < (uint32_t)n
-                         ? __builtin_bit_cast(v4u, __builtin_amdgcn_raw_buffer_load_b128(
-                                                       r1, (rowoff + p * pp) * SZ + 16u * i, 0, 0))
-                         : v4u{0u, 0u, 0u, 0u};
-        }
-#pragma unroll
-        for (int k = 0; k < RB; ++k) {
-            const uint32_t p = base + p0 + (uint32_t)k * ppp;
-            if (chunk_live && p < (uint32_t)n) *(v4u*)(row1 + p * wpb + 16u * i) = buf[k];
-        }
-    }
-    __syncthreads();
-    if (!live) return;
-    const int idx1 = col - d;
-    const bool inb = d != INVALID_I16 && idx1 >= 0 && idx1 < cols;
-    // the right samples from LDS, read in both passes next to their use (as agree_lds_kernel
-    // reads its left tile): plane t at element idx1 + t * wpb / SZ
-    const TIn* rt = (const TIn*)row1 + (inb ? idx1 : 0);
-    const uint32_t ps = wpb / SZ;
-    TPrec corr = (TPrec)__builtin_nan("");
-    if (inb) {
-        uint32_t sl = 0, sr = 0;
-#pragma unroll
-        for (int t = 0; t < MAXN; ++t)
-            if (t < n) {
-                sl += l[t];
-                sr += rt[t * ps];
-                if ((t & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-            }
-        asm volatile("" ::: "memory");
-        const TPrec m0 = div_p((TPrec)sl, (TPrec)n);
-        const TPrec m1 = div_p((TPrec)sr, (TPrec)n);
-        TPrec cov = 0, v0 = 0, v1 = 0;
-#pragma unroll
-        for (int t = 0; t < MAXN; ++t)
-            if (t < n) {
-                const TPrec x0 = (TPrec)l[t] - m0;
-                const TPrec x1 = (TPrec)(uint32_t)rt[t * ps] - m1;
-                cov = fma_p(x0, x1, cov);
-                v0 = fma_p(x0, x0, v0);
-                v1 = fma_p(x1, x1, v1);
-                if ((t & 7) == 7) __builtin_amdgcn_sched_barrier(0);
-            }
-        if (a.has_minvar && (v0 < (TPrec)a.minvar || v1 < (TPrec)a.minvar))
-            corr = (TPrec)-1;
-        else
-            corr = div_p(cov, sqrt_p(v0 * v1));
-        if (corr < (TPrec)a.threshold) d = INVALID_I16;  // NaN passes, as in the reference
-    } else {
-        d = INVALID_I16;
-    }
-    const size_t o = (size_t)row * cols + col;
-    if (a.out_f32)
-        ((float*)a.out)[o] = (float)d;
-    else
-        ((int16_t*)a.out)[o] = (int16_t)d;
-    if (a.corrmap) ((TPrec*)a.corrmap)[o] = corr;
-}
-
 // ------------------------------------------------------------------- dispatch
 
 template <typename TIn, int WORDS, int MAXN>
@@ -903,27 +795,6 @@ hipError_t launch_agree_m(const AgreeArgs& a, hipStream_t st) {
     const size_t sz = sizeof(TIn);
     const bool aligned = ((uintptr_t)a.stack0 % 4 == 0) && (a.row_pitch * sz) % 4 == 0 &&
                          (a.plane_pitch * sz) % 4 == 0;
-    // whole right row in LDS (agree_row_kernel): BICOS_AGREE_ROW=1 (A/B; read per call, so
-    // one test process covers both kernels)
-    const char* row_v = std::getenv("BICOS_AGREE_ROW");
-    const bool row_env = row_v && std::atoi(row_v) != 0;
-    if (aligned && row_env) {
-        const size_t wpb = ((size_t)a.cols * sz + 15) / 16 * 16;
-        const size_t lds = (size_t)a.n * wpb;
-        const int bs = a.cols >= 1024 ? 1024 : (a.cols + 63) / 64 * 64;
-        int rbp = 1;  // the kernel's chunks per plane, rounded up to a power of two
-        while (rbp < (int)(wpb / 16)) rbp *= 2;
-        if (lds <= 160 * 1024 && rbp <= bs) {
-            auto kern = agree_row_kernel<TIn, TPrec, MAXN>;
-            if (lds > 64 * 1024) {
-                const hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-                if (e != hipSuccess) return e;
-            }
-            hipLaunchKernelGGL(kern, dim3((a.cols + bs - 1) / bs, a.rows), dim3(bs), lds, st, a);
-            return hipGetLastError();
-        }
-    }
     if (aligned) {
         // runtime n even for an exact bucket: with a constant n the compiler front-loads
         // the conversions and doubles the VGPRs (49 -> 100 at n = 33)
@@ -1034,7 +905,10 @@ hipError_t launch_consistency(const ConsistencyArgs& a, hipStream_t st) {
 hipError_t launch_reverse_list(const ReverseListArgs& a, hipStream_t st) {
     if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
     if (a.cols > 32767 || a.list_pitch < (size_t)a.cols) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(reverse_list_kernel, dim3(a.rows), dim3(1024), 0, st, a);
+    ReverseListArgs b = a;
+    const char* diag = std::getenv("BICOS_REV_LIST_ALL");  // diagnostic: every k-th col1
+    b.all = diag ? std::max(1, std::atoi(diag)) : 0;
+    hipLaunchKernelGGL(reverse_list_kernel, dim3(b.rows), dim3(1024), 0, st, b);
     return hipGetLastError();
 }
 

@@ -51,6 +51,7 @@ struct ReverseListArgs {
     int* count;             // [rows]
     int rows, cols;
     size_t list_pitch;
+    int all;                // set by launch_reverse_list (BICOS_REV_LIST_ALL=k: every k-th col1)
 };
 hipError_t launch_reverse_list(const ReverseListArgs& a, hipStream_t st);
 

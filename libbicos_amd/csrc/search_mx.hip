@@ -210,6 +210,20 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 // the index ranges above run over i, workgroups past the row's count exit at once, and the
 // block order starts REV_AHEAD columns above the wave's highest entry (a reverse match lies
 // at col0 = col1 + d, d >= 0 in a rectified pair).
+// (row, tile) of a compacted (LIST) launch: grid = 8 x R8 x tiles_per_row, R8 = ceil(rows / 8).
+// XCD x = bid % 8 owns rows [x R8, (x + 1) R8) (a row's workgroups share its right row in
+// that XCD's L2), and within the XCD the order is tile-major: every row's tile 0 first, then
+// every row's tile 1, ... Row-major order put the workgroups past a row's count -- which exit
+// at once -- in a fixed pattern (tiles 2 and 3 of every row at 52 % kept), and the dispatcher
+// then ran the live ones on a fixed subset of the CUs: a 52 % list took as long as the whole
+// row (random u128, profiles/reverse_search_r05.jsonl). Rows >= rows exit.
+__device__ __forceinline__ void list_row_tile(int tiles_per_row, int rows, int& row, int& tile) {
+    const int r8 = (rows + 7) / 8;
+    const int j = blockIdx.x / 8;
+    tile = j / r8;
+    row = (blockIdx.x % 8) * r8 + j % r8;
+}
+
 constexpr int REV_AHEAD = 64;
 template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIST>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KSU >= 4 ? 3 : 4)))
@@ -235,8 +249,12 @@ void search_mx_kernel(SearchArgs a) {
     const int per_xcd = (nwg + 7) / 8;
     int logical = (bid % 8) * per_xcd + bid / 8;
     if (nwg % 8 != 0) logical = bid;
-    const int row = logical / a.tiles_per_row;
-    const int tile = logical % a.tiles_per_row;
+    int row = logical / a.tiles_per_row;
+    int tile = logical % a.tiles_per_row;
+    if constexpr (LIST) {
+        list_row_tile(a.tiles_per_row, a.rows, row, tile);
+        if (row >= a.rows) return;
+    }
     const int c0_base = TAIL ? a.tail_col0 : 0;
 
     const int lane = threadIdx.x & 63;
@@ -783,8 +801,12 @@ void search_pk_kernel(SearchArgs a) {
     const int per_xcd = (nwg + 7) / 8;
     int logical = (bid % 8) * per_xcd + bid / 8;
     if (nwg % 8 != 0) logical = bid;
-    const int row = logical / a.tiles_per_row;
-    const int tile = logical % a.tiles_per_row;
+    int row = logical / a.tiles_per_row;
+    int tile = logical % a.tiles_per_row;
+    if constexpr (LIST) {
+        list_row_tile(a.tiles_per_row, a.rows, row, tile);
+        if (row >= a.rows) return;
+    }
 
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1012,7 +1034,7 @@ hipError_t launch_pk(const SearchArgs& a, int waves, hipStream_t st) {
     if (a.list) {  // compacted col0: workgroups for the whole width, those past the count exit
         SearchArgs b = a;
         b.tiles_per_row = (int)((a.cols + 64L * waves * T - 1) / (64L * waves * T));
-        return launch_pk_grid<WORDS, T, false, true>(b, waves, a.rows * b.tiles_per_row, st);
+        return launch_pk_grid<WORDS, T, false, true>(b, waves, 8 * ((a.rows + 7) / 8) * b.tiles_per_row, st);
     }
     hipError_t e = launch_pk_grid<WORDS, T, false>(a, waves, a.rows * a.tiles_per_row, st);
     if constexpr (T > 1) {
@@ -1089,7 +1111,8 @@ hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     b.tail_T = 0;
     b.tail_col0 = a.cols;
     if (a.list)  // compacted col0: the workgroups past a row's count exit at once
-        return launch_mx_grid<WORDS, KSU, NODUPES, T, KEYS, false, true>(b, waves, a.rows * b.tiles_per_row, st);
+        return launch_mx_grid<WORDS, KSU, NODUPES, T, KEYS, false, true>(
+            b, waves, 8 * ((a.rows + 7) / 8) * b.tiles_per_row, st);
     return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 0>(b, waves, st);
 }
 

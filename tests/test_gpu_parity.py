@@ -253,43 +253,6 @@ def test_agree_window_spans(gpu, oracle, n):
         same(host(corr), rc)
 
 
-# The whole-right-row agree (kernels.hip agree_row_kernel, BICOS_AGREE_ROW=1 -- read per
-# call): the disparity patterns above (negative disparities, matches off the row, NaN
-# correlations), widths that are not a multiple of 16 or of a workgroup, u16 stacks, n past
-# its bucket, and whole frames against the oracle's fixtures
-@pytest.mark.parametrize("n,dt,W", [(2, np.uint8, 1024), (8, np.uint8, 1000), (33, np.uint8, 2048),
-                                    (33, np.uint8, 1030), (17, np.uint16, 777), (40, np.uint8, 2048),
-                                    (65, np.uint8, 600), (12, np.uint16, 3000)])
-@pytest.mark.parametrize("minvar", [None, 2.0])
-def test_agree_row_kernel(gpu, oracle, monkeypatch, n, dt, W, minvar):
-    monkeypatch.setenv("BICOS_AGREE_ROW", "1")
-    H = 8
-    L, R = stereo_stack(n, H, W, dt, dmin=3, drange=40, seed=n + 5)
-    rng = np.random.default_rng(n + W)
-    raw = np.empty((H, W), np.int16)
-    raw[0] = 17
-    raw[1] = 20 + rng.integers(-1, 2, size=W)
-    raw[2] = np.where(np.arange(W) % 64 < 32, 5, 250)
-    raw[3] = rng.integers(-40, W + 40, size=W)              # anything, incl. off-row matches
-    raw[4] = 12
-    raw[4, ::7] = -32768
-    raw[5] = np.arange(W) % 9 - 4                            # negative disparities
-    raw[6] = W - 1                                           # only the last column matches
-    raw[7] = -32768
-    R[:, 0, 40:48] = 9                                       # flat right pixels: NaN correlations
-    mv = None if minvar is None else np.float32(minvar) * np.float32(n)
-    rd, rc = oracle.agree(raw, L, R, 0.5, mv)
-    out, corr = gpu.agree(dev(raw), dev(L), dev(R), 0.5, None if mv is None else float(mv))
-    same(host(out), rd.astype(np.float32))
-    same(host(corr), rc)
-
-
-@pytest.mark.parametrize("name", ["cfg1", "cfg2", "cfg4", "cfg2_u16", "full_n8", "cfg5"])
-def test_full_frame_agree_row(gpu, oracle, monkeypatch, name):
-    monkeypatch.setenv("BICOS_AGREE_ROW", "1")
-    _check_frame(gpu, oracle, name)
-
-
 # n covers exact buckets and padded ones (2, 12, 25, 45, 60: slots n..MAXN-1 are exact
 # no-ops) in both loop structures (pipelined MAXN <= 40, top-of-step above); steps cover
 # 41/20/8 x values, 3 and a single x (step > 2)
