@@ -347,6 +347,15 @@ def main():
                          "match's streams, the int16 landing, the gather timing and the frame "
                          "verification) -- rehearses the RCCL branch on a one-GPU box (not a "
                          "measurement)")
+    ap.add_argument("--gather", default="auto", choices=["auto", "dma", "rccl"],
+                    help="N > 1: how the bands reach rank 0. rccl: one RCCL gather per step (its "
+                         "receive runs on rank 0's compute units, beside rank 0's own band: "
+                         "profiles/root_gather_r05.jsonl); dma: every rank copies its band "
+                         "straight into rank 0's receive slot (IPC-mapped) with hipMemcpyAsync on "
+                         "its own stream -- the copy engines of the sending GPU, nothing on rank "
+                         "0's CUs -- and a one-element RCCL all_reduce per step orders the frame; "
+                         "auto (default): dma when its setup self-test passes on every rank, else "
+                         "rccl")
     ap.add_argument("--band-of", type=int, default=1,
                     help="one process, band 0 of an N-way row split (no gather): the band a "
                          "rank of an N-GPU run computes, for profiling at band sizes")
@@ -470,13 +479,23 @@ def main():
         dbytes = hb * W * (4 if has_corr and not i16 else 2)  # float map only with subpixel
         off = (dbytes + 3) // 4 * 4
         nbytes = off + (hb * W * 4 if has_corr else 0)
-        gdev = dev if nccl else torch.device("cpu")
-        NB = max(2, F)
+        # dma: the band buffers live on the GPU even for a gloo rehearsal (ranks sharing one
+        # GPU); decided with a self-test below (auto), before anything is timed
+        want_dma = args.gather in ("auto", "dma") and world > 1
+        gdev = dev if (nccl or want_dma) else torch.device("cpu")
+        # dma: a slot is rewritten only after the frame two steps back is complete (lag L =
+        # 2), so 2L slots keep every write behind the landing of the frame it replaces
+        NB = max(4, F) if want_dma else max(2, F)
         sends = [torch.zeros(nbytes, dtype=torch.uint8, device=gdev) for _ in range(NB)]
         recv_all = [torch.empty((world, nbytes), dtype=torch.uint8, device=gdev) if rank == 0
                     else None for _ in range(NB)]
         recvs = [list(r.unbind(0)) if r is not None else None for r in recv_all]
         pending = [None] * NB
+        dma = setup_dma_gather(args, dist, torch, dev, nccl, rank, world, recv_all, sends,
+                               nbytes) if want_dma else None
+        if dma is None and want_dma and not nccl:
+            # (the rccl-form rehearsal over gloo moves host buffers)
+            raise SystemExit("--gather dma setup failed on a gloo rehearsal")
         # rank 0: the float32 disparity frame of each gather slot (one per slot,
         # so a stale or misordered landing cannot hide behind a shared buffer)
         frame_disps = [torch.empty((world, hb, W), dtype=torch.float32, device=gdev)
@@ -495,6 +514,23 @@ def main():
             pending[i] = None
             if rank == 0 and i16:
                 frame_disps[i].copy_(disp_view(recv_all[i]))
+
+        def dma_step(k, f):
+            # lag 2: the frame of step k-2 is complete everywhere before step k writes (rank 0
+            # lands it first); see setup_dma_gather for why every write is then safe
+            i = k % NB
+            j = k - 2
+            if j >= 0 and pending[j % NB] is not None:
+                land(j % NB)
+            if rank == 0:
+                engines[f].match(s0, s1, mcfg, out=disp_view(recv_all[i][0])[:rows],
+                                 corrmap=corr_view(recv_all[i][0])[:rows] if has_corr else None)
+            else:
+                buf = sends[i]
+                engines[f].match(s0, s1, mcfg, out=disp_view(buf)[:rows],
+                                 corrmap=corr_view(buf)[:rows] if has_corr else None)
+                dma["copy"](i, streams[f])
+            pending[i] = dma["signal"](i, streams[f])
     state = {"k": 0}
 
     # --root-load: the bytes rank 0 of an N-way run receives per step (the other bands'
@@ -505,7 +541,6 @@ def main():
             raise SystemExit("--root-load rehearses rank 0 of --band-of N (one process)")
         bpp = (2 if (i16 or not has_corr) else 4) + (4 if has_corr else 0)
         ing = (args.band_of - 1) * band_height(H, args.band_of) * W * bpp
-        ing = (ing + 3) // 4 * 4
         ing = (ing + 15) // 16 * 16
         load = {"mode": args.root_load, "bytes_per_step": ing, "issued": 0, "skipped": 0,
                 "dst": torch.empty(ing // 4, dtype=torch.int32, device=dev),
@@ -560,6 +595,9 @@ def main():
                 engines[f].match(s0, s1, mcfg, out=outs[f], corrmap=corrs[f])
                 if timed_load:
                     issue_load(k)
+                return
+            if dma is not None:
+                dma_step(k, f)
                 return
             i = k % NB
             if pending[i] is not None:
@@ -621,7 +659,10 @@ def main():
     gather_info = None
     verify = None
     if gather:
-        gather_info = time_gather(dist, torch, dev, nccl, rank, sends[0], recvs[0], nbytes, world)
+        if dma is not None:
+            gather_info = time_dma_exchange(dist, torch, dev, rank, world, dma, streams[0], nbytes)
+        else:
+            gather_info = time_gather(dist, torch, dev, nccl, rank, sends[0], recvs[0], nbytes, world)
         if not args.no_verify_gather:
             verify = verify_gather(args, C, dist, torch, np, dev, nccl, rank, world, eng, mcfg,
                                    step, drain, NB, recv_all, frame_disps, disp_view, corr_view,
@@ -663,6 +704,11 @@ def main():
         if gather and args.gather_rehearsal:
             par = ("rehearsal: the row-band gather path on a 1-rank %s process group (self-"
                    "gather; not a measurement)" % ("RCCL" if nccl else "gloo"))
+        elif gather and dma is not None:
+            par = ("row-bands x%d + copy-engine gather over xGMI (hipMemcpyAsync into rank 0's "
+                   "IPC-mapped slots, RCCL all_reduce per step)" % world if nccl else
+                   "gloo rehearsal: row-bands x%d + copy-engine gather (IPC), ranks sharing %d "
+                   "GPU(s) (not a measurement)" % (world, ndev))
         elif gather:
             par = ("row-bands x%d + RCCL gather over xGMI" % world if nccl else
                    "gloo rehearsal: row-bands x%d + gloo gather, ranks sharing %d GPU(s) "
@@ -729,6 +775,117 @@ def main():
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def setup_dma_gather(args, dist, torch, dev, nccl, rank, world, recv_all, sends, nbytes):
+    """The copy-engine gather (--gather dma|auto). Rank 0 shares its receive slots
+    (recv_all[i], [world, nbytes] bytes on its GPU) through CUDA/HIP IPC (torch's own tensor
+    sharing: the handles go out with broadcast_object_list); every other rank maps them and,
+    per step, copies its packed band into its row of the slot with ONE hipMemcpyAsync on its
+    own stream -- the sending GPU's copy engines over xGMI, nothing on rank 0's CUs (an RCCL
+    gather receives on them: profiles/root_gather_r05.jsonl) -- then joins a one-element
+    all_reduce on that stream (RCCL: stream-ordered behind the copy on every rank, so its
+    completion on rank 0 means every band has landed). Slot reuse (bench.main dma_step): step
+    k first waits for the all_reduce of step k-2 (rank 0 then lands frame k-2); with NB >= 4
+    slots, slot k % NB last held frame k-NB, landed at step k-NB+2 <= k-2 before rank 0's
+    all_reduce of that step, which step k has waited for.
+
+    A self-test (each rank writes a pattern into its row of slot 0, rank 0 checks every row)
+    runs first; any failure on any rank returns None on every rank and the RCCL gather is used
+    (--gather auto), or exits (--gather dma). Returns {"copy", "signal", "remote"}."""
+    import ctypes
+    ok = True
+    why = ""
+    remote = None
+    copy_fn = None
+    try:
+        from torch.multiprocessing.reductions import rebuild_cuda_tensor, reduce_tensor
+        objs = [reduce_tensor(r)[1] if rank == 0 else None for r in recv_all]
+    except Exception as ex:  # noqa: BLE001 -- any failure falls back to the RCCL gather
+        ok, why, objs = False, "share: %s" % ex, [None] * len(recv_all)
+    flag = torch.tensor([1.0 if ok else 0.0], device=dev if nccl else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    if flag.item() == 1.0:
+        dist.broadcast_object_list(objs, src=0)
+        try:
+            if rank != 0:
+                remote = [rebuild_cuda_tensor(*o) for o in objs]
+            hip = ctypes.CDLL("libamdhip64.so")
+            hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_int, ctypes.c_void_p]
+            hip.hipMemcpyAsync.restype = ctypes.c_int
+
+            def copy_fn(i, stream):
+                rc = hip.hipMemcpyAsync(remote[i][rank].data_ptr(), sends[i].data_ptr(), nbytes,
+                                        3, stream.cuda_stream)  # hipMemcpyDeviceToDevice
+                if rc != 0:
+                    raise RuntimeError("hipMemcpyAsync (dma gather) failed: %d" % rc)
+            # self-test: a rank-specific pattern through slot 0
+            torch.cuda.synchronize(dev)
+            if rank != 0:
+                sends[0].fill_(rank * 37 % 251 + 1)
+                st = torch.cuda.current_stream(dev)
+                copy_fn(0, st)
+                st.synchronize()
+        except Exception as ex:  # noqa: BLE001
+            ok, why = False, "map / copy: %s" % ex
+    else:
+        ok = False
+    flag = torch.tensor([1.0 if ok else 0.0], device=dev if nccl else "cpu")
+    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+    ok = flag.item() == 1.0
+    if ok and rank == 0:
+        torch.cuda.synchronize(dev)
+        for r in range(1, world):
+            if not bool((recv_all[0][r] == (r * 37 % 251 + 1)).all().item()):
+                ok, why = False, "self-test: rank %d's row did not land" % r
+                break
+    flag = torch.tensor([1.0 if ok else 0.0], device=dev if nccl else "cpu")
+    dist.broadcast(flag, src=0)
+    ok = ok and flag.item() == 1.0 if rank == 0 else flag.item() == 1.0
+    if not ok:
+        if args.gather == "dma":
+            raise SystemExit("--gather dma: setup failed (%s)" % (why or "on another rank"))
+        if rank == 0:
+            print("gather: copy-engine setup failed (%s); using the RCCL gather" %
+                  (why or "on another rank"), file=sys.stderr)
+        return None
+    sigs = [torch.zeros(1, device=dev if nccl else "cpu") for _ in range(len(recv_all))]
+
+    def signal(i, stream):
+        if nccl:  # stream-ordered behind the copy (we are inside torch.cuda.stream(stream))
+            return dist.all_reduce(sigs[i], async_op=True)
+        stream.synchronize()  # gloo (rehearsal): the copy is done before the host joins
+        return dist.all_reduce(sigs[i], async_op=True)
+    return {"copy": copy_fn, "signal": signal, "remote": remote}
+
+
+def time_dma_exchange(dist, torch, dev, rank, world, dma, stream, nbytes, reps=10):
+    """The copy-engine exchange alone (untimed region): per rep, a barrier, then every rank
+    but 0 copies one band into rank 0's slot 0 and all ranks join the signalling all_reduce;
+    host wall time until it completes on this rank, median, max over ranks."""
+    ts = []
+    for _ in range(reps):
+        dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        with torch.cuda.stream(stream):
+            if rank != 0:
+                dma["copy"](0, stream)
+            w = dma["signal"](0, stream)
+        w.wait()
+        torch.cuda.synchronize(dev)
+        ts.append(time.perf_counter() - t0)
+    t = sorted(ts)[len(ts) // 2]
+    tt = torch.tensor([t], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    t = float(tt.item())
+    return {"mode": "dma", "ms_per_exchange": round(t * 1e3, 4), "bytes_per_rank": nbytes,
+            "bytes_to_root": nbytes * (world - 1),
+            "GBps_into_root": round(nbytes * (world - 1) / t / 1e9, 1),
+            "what": "every rank but 0 copies its packed band into rank 0's IPC-mapped slot "
+                    "(hipMemcpyAsync on its own stream) + one-element all_reduce, host wall time "
+                    "incl. launch, median of %d, max over ranks" % reps}
 
 
 def time_gather(dist, torch, dev, nccl, rank, send, recv, nbytes, world, reps=10):

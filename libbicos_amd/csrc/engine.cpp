@@ -425,39 +425,12 @@ int match_host(bicos_engine* e, const void* const* p0, const size_t* steps0,
         e->pinned_bytes = (size_t)K * band_bytes;
     }
     const size_t disp_bytes = (size_t)rows * cols * dsz;
-    const size_t corr_bytes = corr ? (size_t)rows * cols * csz : 0;
     while ((int)e->events.size() < B) {
         hipEvent_t ev;
         rc = check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
         if (rc) return rc;
         e->events.push_back(ev);
     }
-    // Band-wise downloads (BICOS_HOST_DL=0: one download of the whole maps at the end, the
-    // round-4 form): each band's maps go down into pinned memory right after its match,
-    // while the later bands still upload (PCIe is full duplex), and the pool copies each
-    // band to the caller once it has landed. The whole-map download at the end was 0.45 ms
-    // of an otherwise idle link at cfg2 (profiles/host_path_r05.jsonl).
-    const char* dl_env = std::getenv("BICOS_HOST_DL");
-    const bool band_dl = B > 1 && !(dl_env && std::atoi(dl_env) == 0);
-    if (band_dl) {
-        if (e->pinned_out_bytes < disp_bytes + corr_bytes) {
-            if (e->pinned_out) (void)hipHostFree(e->pinned_out);
-            e->pinned_out = nullptr;
-            e->pinned_out_bytes = 0;
-            rc = check_hip(hipHostMalloc(&e->pinned_out, disp_bytes + corr_bytes, hipHostMallocDefault),
-                           "hipHostMalloc(map staging)");
-            if (rc) return rc;
-            e->pinned_out_bytes = disp_bytes + corr_bytes;
-        }
-        while ((int)e->dl_events.size() < B) {
-            hipEvent_t ev;
-            rc = check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-            if (rc) return rc;
-            e->dl_events.push_back(ev);
-        }
-    }
-    char* host_disp = band_dl ? (char*)e->pinned_out : nullptr;
-    char* host_corr = band_dl && corr ? (char*)e->pinned_out + disp_bytes : nullptr;
     if (!e->pool) {
         // gather threads (BICOS_HOST_THREADS, default 8): the gathers compete with the DMA
         // for host memory bandwidth; 16 threads measured slower than 3-8 (tools/host_bench.py)
@@ -530,43 +503,13 @@ int match_host(bicos_engine* e, const void* const* p0, const size_t* steps0,
                               (size_t)br * cols, depth, cfg, has_nxcorr, threshold,
                               dev_disp + (size_t)r0 * cols * dsz,
                               dev_corr ? dev_corr + (size_t)r0 * cols * csz : nullptr, cs);
-        if (!rc && band_dl) {
-            const size_t od = (size_t)r0 * cols * dsz, oc = (size_t)r0 * cols * csz;
-            rc = check_hip(hipMemcpyAsync(host_disp + od, dev_disp + od, (size_t)br * cols * dsz,
-                                          hipMemcpyDeviceToHost, cs), "download");
-            if (!rc && corr)
-                rc = check_hip(hipMemcpyAsync(host_corr + oc, dev_corr + oc, (size_t)br * cols * csz,
-                                              hipMemcpyDeviceToHost, cs), "download");
-            if (!rc) rc = check_hip(hipEventRecord(e->dl_events[b], cs), "hipEventRecord");
-        }
     }
     stamp("bands queued", B);
     if (trace) {
         (void)hipStreamSynchronize(cs);
         stamp("bands matched", B);
     }
-    if (!rc && band_dl) {
-        // each band to the caller as soon as it has landed (the pool splits it in chunks)
-        for (int b = 0; b < B && !rc; ++b) {
-            rc = check_hip(hipEventSynchronize(e->dl_events[b]), "hipEventSynchronize");
-            if (rc) break;
-            const int r0 = b * band_rows;
-            const int br = std::min(band_rows, rows - r0);
-            const size_t od = (size_t)r0 * cols * dsz, nd = (size_t)br * cols * dsz;
-            const size_t oc = (size_t)r0 * cols * csz, nc = (size_t)br * cols * csz;
-            constexpr int CH = 8;
-            const std::function<void(int)> put = [&](int i) {
-                const bool c = i >= CH;
-                const int k = c ? i - CH : i;
-                const size_t n_all = c ? nc : nd;
-                const size_t a = n_all * k / CH, z = n_all * (k + 1) / CH;
-                if (z > a)
-                    std::memcpy((c ? (char*)corr + oc : (char*)disp + od) + a,
-                                (c ? host_corr + oc : host_disp + od) + a, z - a);
-            };
-            e->pool->run(corr ? 2 * CH : CH, put);
-        }
-    } else if (!rc) {
+    if (!rc) {
         rc = check_hip(hipMemcpyAsync(disp, dev_disp, disp_bytes, hipMemcpyDeviceToHost, cs),
                        "download");
         if (!rc && corr)
@@ -678,9 +621,7 @@ void bicos_engine_destroy(bicos_engine* e) {
     if (e->stage) (void)hipFreeAsync(e->stage, e->own_stream);
     (void)hipStreamSynchronize(e->own_stream);
     if (e->pinned) (void)hipHostFree(e->pinned);
-    if (e->pinned_out) (void)hipHostFree(e->pinned_out);
     for (hipEvent_t ev : e->events) (void)hipEventDestroy(ev);
-    for (hipEvent_t ev : e->dl_events) (void)hipEventDestroy(ev);
     e->pool.reset();
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);

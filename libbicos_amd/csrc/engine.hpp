@@ -64,11 +64,6 @@ struct bicos_engine {
     void* pinned = nullptr;  // K input band slots
     size_t pinned_bytes = 0;
     std::vector<hipEvent_t> events;
-    // the maps come down band by band into pinned memory while later bands upload (PCIe is
-    // full duplex), then the pool copies them to the caller: one event per band
-    void* pinned_out = nullptr;
-    size_t pinned_out_bytes = 0;
-    std::vector<hipEvent_t> dl_events;
     std::unique_ptr<bicos_impl::HostPool> pool;
 };
 

@@ -210,18 +210,30 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 // the index ranges above run over i, workgroups past the row's count exit at once, and the
 // block order starts REV_AHEAD columns above the wave's highest entry (a reverse match lies
 // at col0 = col1 + d, d >= 0 in a rectified pair).
-// (row, tile) of a compacted (LIST) launch: grid = 8 x R8 x tiles_per_row, R8 = ceil(rows / 8).
-// XCD x = bid % 8 owns rows [x R8, (x + 1) R8) (a row's workgroups share its right row in
-// that XCD's L2), and within the XCD the order is tile-major: every row's tile 0 first, then
-// every row's tile 1, ... Row-major order put the workgroups past a row's count -- which exit
-// at once -- in a fixed pattern (tiles 2 and 3 of every row at 52 % kept), and the dispatcher
-// then ran the live ones on a fixed subset of the CUs: a 52 % list took as long as the whole
-// row (random u128, profiles/reverse_search_r05.jsonl). Rows >= rows exit.
+// (row, tile) of a compacted (LIST) launch: grid = 8 x ceil(R8 / G) G x tiles_per_row, R8 =
+// ceil(rows / 8), G = LIST_GROUP rows. XCD x = bid % 8 owns rows [x R8, (x + 1) R8), and
+// within the XCD the order is tile-major per group of G rows: the group's tile 0 workgroups,
+// then its tile 1 workgroups, ... Row-major order put the workgroups past a row's count --
+// which exit at once -- in a fixed pattern (tiles 2 and 3 of every row at 52 % kept), and the
+// dispatcher then ran the live ones on a fixed subset of the CUs: a 52 % list took as long
+// as the whole row (random u128, profiles/reverse_search_r05.jsonl). Tile-major over all of
+// the XCD's rows fixed that but put a row's workgroups hundreds of workgroups apart, past
+// the XCD's L2 (cfg4's reverse search +4.5 %); a group of G = 32 rows x 2 tiles is what an
+// XCD holds at once (32 CUs x 2 workgroups), so a row's workgroups run together again.
+// Rows past the XCD's range (or past rows) exit.
+constexpr int LIST_GROUP = 32;
 __device__ __forceinline__ void list_row_tile(int tiles_per_row, int rows, int& row, int& tile) {
     const int r8 = (rows + 7) / 8;
     const int j = blockIdx.x / 8;
-    tile = j / r8;
-    row = (blockIdx.x % 8) * r8 + j % r8;
+    const int per_group = LIST_GROUP * tiles_per_row;
+    const int g = j / per_group, w = j % per_group;
+    tile = w / LIST_GROUP;
+    const int r = g * LIST_GROUP + w % LIST_GROUP;  // row within the XCD's range
+    row = r < r8 ? (blockIdx.x % 8) * r8 + r : rows;
+}
+inline int list_grid(int rows, int tiles_per_row) {
+    const int r8 = (rows + 7) / 8;
+    return 8 * ((r8 + LIST_GROUP - 1) / LIST_GROUP) * LIST_GROUP * tiles_per_row;
 }
 
 constexpr int REV_AHEAD = 64;
@@ -1034,7 +1046,7 @@ hipError_t launch_pk(const SearchArgs& a, int waves, hipStream_t st) {
     if (a.list) {  // compacted col0: workgroups for the whole width, those past the count exit
         SearchArgs b = a;
         b.tiles_per_row = (int)((a.cols + 64L * waves * T - 1) / (64L * waves * T));
-        return launch_pk_grid<WORDS, T, false, true>(b, waves, 8 * ((a.rows + 7) / 8) * b.tiles_per_row, st);
+        return launch_pk_grid<WORDS, T, false, true>(b, waves, list_grid(a.rows, b.tiles_per_row), st);
     }
     hipError_t e = launch_pk_grid<WORDS, T, false>(a, waves, a.rows * a.tiles_per_row, st);
     if constexpr (T > 1) {
@@ -1112,7 +1124,7 @@ hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     b.tail_col0 = a.cols;
     if (a.list)  // compacted col0: the workgroups past a row's count exit at once
         return launch_mx_grid<WORDS, KSU, NODUPES, T, KEYS, false, true>(
-            b, waves, 8 * ((a.rows + 7) / 8) * b.tiles_per_row, st);
+            b, waves, list_grid(a.rows, b.tiles_per_row), st);
     return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 0>(b, waves, st);
 }
 

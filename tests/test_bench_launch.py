@@ -45,14 +45,17 @@ def test_failing_rank_fails_the_launch():
 
 
 @pytest.mark.gpu
-def test_two_rank_gloo_line_has_every_field():
+@pytest.mark.parametrize("gather", ["rccl", "dma"])
+def test_two_rank_gloo_line_has_every_field(gather):
     """The N>1 bench line is self-contained: two gloo ranks sharing the
     box's GPU run the row-band path; rank 0's line carries the search roofline with its PMC
     traffic lookup, the gather timed on its own, the gathered frames verified against the
     oracle's whole-frame hash, and a "gloo rehearsal" label (the CPU baseline is an N = 1
-    field, null here)."""
-    p = _run(["--gpus", "2", "--backend", "gloo", "--steps", "3", "--warmup", "1",
-              "--cpu-seconds", "2", "--kernel-reps", "2", "--no-host-path"], timeout=110)
+    field, null here). gather=dma: the copy-engine gather (rank 1 maps rank 0's receive
+    slots through IPC and copies its band into them with hipMemcpyAsync), the same check."""
+    p = _run(["--gpus", "2", "--backend", "gloo", "--gather", gather, "--steps", "3",
+              "--warmup", "1", "--cpu-seconds", "2", "--kernel-reps", "2", "--no-host-path"],
+             timeout=110)
     assert p.returncode == 0, p.stderr[-3000:]
     lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, p.stdout
@@ -66,9 +69,15 @@ def test_two_rank_gloo_line_has_every_field():
     assert "traffic" in roof and roof["traffic_source"]
     assert roof["match_hbm_read"]["peak_GBps"] == 16000.0
     g = d["gather"]
-    assert g["ms"] > 0 and g["bytes_to_root"] == g["bytes_per_rank"]
+    if gather == "dma":
+        assert "copy-engine" in d["config"]["parallelism"]
+        assert g["mode"] == "dma" and g["ms_per_exchange"] > 0
+    else:
+        assert "gloo gather" in d["config"]["parallelism"]
+        assert g["ms"] > 0
+    assert g["bytes_to_root"] == g["bytes_per_rank"]
     v = d["verify_gather"]
-    assert v["ok"] and v["slots"] >= 2 and v["bands"] == 2
+    assert v["ok"] and v["slots"] >= (4 if gather == "dma" else 2) and v["bands"] == 2
     assert "frames.json" in v["check"]
 
 

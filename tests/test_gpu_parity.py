@@ -708,6 +708,81 @@ def test_double_precision(gpu, oracle):
     assert np.abs(c32[rr, cc][fin] - ref[fin]).max() < FLOAT_TOL
 
 
+def _subpixel_f64(L, R, raw, thr, step, minvar):
+    """float64 restatement of the DOUBLE subpixel refine (reference agree.cuh:161-259 with
+    TPrecision = double): the quadratic interpolation stays float32 exactly as in the float
+    path (oracle/ref_numpy.py agree_subpixel), the correlation and its argmax are float64
+    (numpy, no fma: compare within 1e-12), min-variance on the float64 variances."""
+    from oracle import ref_numpy as N
+    n, H, W = L.shape
+    f32 = np.float32
+    out = np.full((H, W), np.nan, np.float32)
+    corr = np.full((H, W), np.nan, np.float64)
+
+    def nxc64(a, b):
+        a = a.astype(np.float64)
+        b = b.astype(np.float64)
+        a = a - a.sum(0) / n
+        b = b - b.sum(0) / n
+        v0, v1 = (a * a).sum(0), (b * b).sum(0)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            r = (a * b).sum(0) / np.sqrt(v0 * v1)
+        if minvar is not None:
+            r = np.where((v0 < minvar) | (v1 < minvar), -1.0, r)
+        return r
+    d = raw.astype(np.int64)
+    rr, cc = np.nonzero(raw != -32768)
+    col1 = cc - d[rr, cc]
+    keep = (col1 >= 0) & (col1 < W)
+    rr, cc, col1 = rr[keep], cc[keep], col1[keep]
+    edge = (col1 == 0) | (col1 == W - 1)
+    er, ec, e1 = rr[edge], cc[edge], col1[edge]
+    if er.size:
+        v = nxc64(L[:, er, ec], R[:, er, e1])
+        corr[er, ec] = v
+        ok = ~(v < thr)
+        out[er[ok], ec[ok]] = d[er[ok], ec[ok]].astype(np.float32)
+    ir, ic, i1 = rr[~edge], cc[~edge], col1[~edge]
+    y0 = R[:, ir, i1 - 1].astype(np.float32)
+    y1 = R[:, ir, i1].astype(np.float32)
+    y2 = R[:, ir, i1 + 1].astype(np.float32)
+    A = (f32(0.5) * ((y0 - f32(2.0) * y1).astype(np.float32) + y2)).astype(np.float32)
+    B = (f32(0.5) * (-R[:, ir, i1 - 1].astype(np.int64) + R[:, ir, i1 + 1].astype(np.int64)
+                     ).astype(np.float32)).astype(np.float32)
+    best_x = np.zeros(ir.size, np.float32)
+    best = np.full(ir.size, -1.0)
+    for x in N.x_steps(step):
+        ax = (A * x).astype(np.float32)
+        v = (((ax * x).astype(np.float32) + (B * x).astype(np.float32)).astype(np.float32)
+             + y1).astype(np.float32)
+        c = nxc64(L[:, ir, ic], N._narrow(v, L.dtype))
+        win = best < c
+        best_x = np.where(win, x, best_x)
+        best = np.where(win, c, best)
+    corr[ir, ic] = best
+    ok = ~(best < thr)
+    out[ir[ok], ic[ok]] = (d[ir[ok], ic[ok]].astype(np.float32) - best_x[ok]).astype(np.float32)
+    return out, corr
+
+
+# Precision::DOUBLE subpixel at the exact-kernel depths n = 6 / 10 / 12 (the reference's
+# integration and kernel-bench depths; ADVICE r04: only the float path was pinned there)
+@pytest.mark.parametrize("n", [6, 10, 12])
+@pytest.mark.parametrize("step,minvar", [(0.25, None), (0.1, 2.0)])
+def test_double_subpixel_exact_depths(gpu, oracle, n, step, minvar):
+    L, R = stereo_stack(n, 6, 300, dmin=3, drange=30, seed=n + 17)
+    raw, _ = oracle.match(L, R, oracle.OracleConfig(nxcorr_threshold=None, mode=1))
+    mv = None if minvar is None else float(np.float32(minvar) * np.float32(n))
+    out, corr = gpu.agree(dev(raw), dev(L), dev(R), 0.5, mv, step=step, precision=1)
+    ref_d, ref_c = _subpixel_f64(L, R, raw, 0.5, step, mv)
+    got_c = host(corr)
+    assert got_c.dtype == np.float64
+    fin = np.isfinite(ref_c)
+    assert (np.isfinite(got_c) == fin).all()
+    assert np.abs(got_c[fin] - ref_c[fin]).max() < 1e-12
+    same(host(out), ref_d)
+
+
 def test_deterministic(gpu):
     L, R = stereo_stack(33, 32, 1024)
     a = gpu_match(gpu, L, R, nxcorr_threshold=0.9, subpixel_step=0.1)

@@ -167,6 +167,10 @@ for step in "$@"; do
                 run pmc_${c}_b${nb}_sq 150 timeout -s KILL 140 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VMEM_RD SQ_INSTS_VALU GRBM_GUI_ACTIVE TA_TA_BUSY_sum TD_TD_BUSY_sum -d gpurun_out/pmc/${c}__b${nb}__sq -o run --output-format csv -- python bench.py --config $c --band-of $nb --steps 3 --warmup 1 --spinup-ms 0 --kernel-reps 0 --inflight 1 --no-cpu-baseline --no-host-path
                 run pmc_${c}_b${nb}_mem 150 timeout -s KILL 140 rocprofv3 --pmc TCP_TCC_READ_REQ_LATENCY_sum TCP_TCC_READ_REQ_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCC_HIT_sum TCC_MISS_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum TD_TC_STALL_sum TD_SPI_STALL_sum GRBM_GUI_ACTIVE SQ_WAVES -d gpurun_out/pmc/${c}__b${nb}__mem -o run --output-format csv -- python bench.py --config $c --band-of $nb --steps 3 --warmup 1 --spinup-ms 0 --kernel-reps 0 --inflight 1 --no-cpu-baseline --no-host-path
             done ;;
+        dmag)  # the copy-engine gather rehearsed with gloo ranks sharing the one GPU (IPC-mapped slots, hipMemcpyAsync), 2 and 3 ranks, + the rccl-form rehearsal
+            run dmag2 600 python bench.py --gpus 2 --backend gloo --gather dma --steps 5 --warmup 1 --no-cpu-baseline --no-host-path
+            run dmag3 600 python bench.py --gpus 3 --backend gloo --gather dma --config cfg3 --steps 5 --warmup 1 --no-cpu-baseline --no-host-path
+            run rcclg2 600 python bench.py --gpus 2 --backend gloo --gather rccl --steps 5 --warmup 1 --no-cpu-baseline --no-host-path ;;
         benchg2)  # the N=2 path rehearsed with gloo ranks sharing the one GPU (all line fields)
             run benchg2 600 python bench.py --gpus 2 --backend gloo --steps 5 --warmup 1 --cpu-seconds 4 ;;
         tunepipe)  # search geometries that leave wave slots for the other frames' HBM stages
