@@ -211,6 +211,10 @@ for step in "$@"; do
             for k in 1 2 4 8; do
                 BICOS_REV_LIST_ALL=$k run revstride_$k 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revstride_$k -o run --output-format csv -- python tools/random_search_bench.py --words 4 --inputs random_u128 --reps 3
             done ;;
+        revprof4)  # cfg4 kernel stats one frame at a time: compacted reverse, full reverse, every col1 through the list
+            run revprof4_kept 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof4_kept -o run --output-format csv -- python bench.py --config cfg4 --steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --no-host-path --kernel-reps 0
+            BICOS_REV_FULL=1 run revprof4_full 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof4_full -o run --output-format csv -- python bench.py --config cfg4 --steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --no-host-path --kernel-reps 0
+            BICOS_REV_LIST_ALL=1 run revprof4_all 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof4_all -o run --output-format csv -- python bench.py --config cfg4 --steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --no-host-path --kernel-reps 0 ;;
         revab)  # Consistency's reverse search over the kept col1 vs the full reverse pass (BICOS_REV_FULL=1)
             run randsearch_kept 600 python tools/random_search_bench.py --words 1,2,4 --out gpurun_out/random_search_kept.jsonl
             BICOS_REV_FULL=1 run randsearch_full 600 python tools/random_search_bench.py --words 1,2,4 --out gpurun_out/random_search_full.jsonl
