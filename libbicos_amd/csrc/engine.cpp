@@ -161,6 +161,9 @@ static int required_bits(int n, int mode) { return mode ? n * n - 2 * n + 3 : 4 
 // as compacted col0 entries; rev elsewhere is left unwritten and never read. Periodic
 // inputs whose forward search keeps nothing skip the reverse pass almost entirely.
 // BICOS_REV_FULL=1 (A/B) and the VALU search run the full reverse pass.
+// the reverse list's row pitch: whole 16-byte rows (reverse_list_kernel stores them so)
+static size_t list_pitch(int cols) { return ((size_t)cols + 7) / 8 * 8; }
+
 template <typename F>
 static int reverse_search(bool mx, int rows, int cols, const int16_t* fwd, int16_t* list,
                           int* count, hipStream_t st, F&& run) {
@@ -169,7 +172,7 @@ static int reverse_search(bool mx, int rows, int cols, const int16_t* fwd, int16
         return v && std::atoi(v) != 0;
     }();
     if (!mx || full) return run(nullptr, nullptr);
-    bicos_hip::ReverseListArgs la{fwd, list, count, rows, cols, (size_t)cols};
+    bicos_hip::ReverseListArgs la{fwd, list, count, rows, cols, list_pitch(cols)};
     int rc = check_hip(bicos_hip::launch_reverse_list(la, st), "reverse list launch");
     return rc ? rc : run(list, count);
 }
@@ -234,7 +237,9 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     const size_t desc_bytes = align_up((size_t)rows * dpitch * 4);
     const size_t map16 = align_up((size_t)rows * cols * 2);
     const size_t counts = align_up((size_t)rows * 4);
-    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) + (consistency ? 3 * map16 + counts : 0);
+    const size_t lbytes = align_up((size_t)rows * list_pitch(cols) * 2);
+    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) +
+                  (consistency ? 2 * map16 + lbytes + counts : 0);
     int rc = reserve(e->ws, e->ws_bytes, need, e->device, st, e->ws_ready);
     if (rc) return rc;
     // order against earlier users of ws / stage on other streams; mark our use on exit
@@ -255,7 +260,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     int16_t* fwd = consistency ? (int16_t*)p : nullptr;
     int16_t* rev = consistency ? (int16_t*)(p + map16) : nullptr;
     int16_t* rlist = consistency ? (int16_t*)(p + 2 * map16) : nullptr;
-    int* rcount = consistency ? (int*)(p + 3 * map16) : nullptr;
+    int* rcount = consistency ? (int*)(p + 2 * map16 + lbytes) : nullptr;
 
     // 1. descriptor_transform, both stacks in one launch (cpu.cpp:50-59)
     bicos_hip::TransformArgs ta{s0, s1, d0, d1, n, rows, cols, row_pitch, plane_pitch, dpitch, 0, span};
@@ -271,7 +276,7 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
         bicos_hip::SearchArgs sa{a0, a1, out, rows, cols, dpitch, (size_t)cols, out_mode, 0, 0, 0};
         sa.list = list;
         sa.lcount = lcount;
-        sa.list_pitch = (size_t)cols;
+        sa.list_pitch = list_pitch(cols);
         if (mx)
             return check_hip(bicos_hip::launch_search_mx(
                                  sa, mx_geometry(e, rows, cols, words, used_bits(n, mode)), words, nd, st),
@@ -783,8 +788,9 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     if (!e) return fail(BICOS_E_ARG, "consistency search needs an engine workspace");
     std::lock_guard<std::mutex> lk(e->lock);  // the workspace may be shared (default engine)
     const size_t map16 = align_up((size_t)rows * cols * 2);
-    int rc = reserve(e->ws, e->ws_bytes, 3 * map16 + align_up((size_t)rows * 4), e->device, st,
-                     e->ws_ready);
+    const size_t lbytes = align_up((size_t)rows * list_pitch(cols) * 2);
+    int rc = reserve(e->ws, e->ws_bytes, 2 * map16 + lbytes + align_up((size_t)rows * 4), e->device,
+                     st, e->ws_ready);
     if (rc) return rc;
     rc = check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent");
     if (rc) return rc;
@@ -796,7 +802,7 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     int16_t* fwd = (int16_t*)e->ws;
     int16_t* rev = (int16_t*)((char*)e->ws + map16);
     int16_t* rlist = (int16_t*)((char*)e->ws + 2 * map16);
-    int* rcount = (int*)((char*)e->ws + 3 * map16);
+    int* rcount = (int*)((char*)e->ws + 2 * map16 + lbytes);
     bicos_hip::SearchArgs fa{desc0, desc1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
     bicos_hip::SearchArgs ra{desc1, desc0, rev, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
     if (mx) {
@@ -807,7 +813,7 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
                             [&](const int16_t* l, const int* c) {
                                 ra.list = l;
                                 ra.lcount = c;
-                                ra.list_pitch = (size_t)cols;
+                                ra.list_pitch = list_pitch(cols);
                                 return check_hip(bicos_hip::launch_search_mx(ra, gm, words, nodupes, st),
                                                  "reverse search launch");
                             });

@@ -465,12 +465,14 @@ __global__ __launch_bounds__(256) void consistency_kernel(ConsistencyArgs a) {
 // reverse search runs only where the forward one found a valid match): one 256-thread
 // workgroup per row marks the col1 some forward match chose in an LDS bitmap (<= 1024 words:
 // cols <= 32767), then each thread takes 4 consecutive words -- an exclusive scan of their
-// popcounts gives its first list slot -- and writes their marked col1 in ascending order.
-// (256 threads, 4 words each: several rows resident per CU; the 1024-thread form took 22 us
-// at 3300 x 2200, latency-bound.)
+// popcounts gives its first list slot -- and writes their marked col1 in ascending order into
+// an LDS copy of the list (dynamic, cols x 2 bytes), which the workgroup stores with 16-byte
+// writes. (Scattered 2-byte global stores, one per marked column, took 23.7 us at cfg4:
+// every store instruction touched ~64 cache lines.)
 __global__ __launch_bounds__(256) void reverse_list_kernel(ReverseListArgs a) {
     __shared__ uint32_t mark[1024];
     __shared__ int wsum[4];
+    extern __shared__ __attribute__((aligned(16))) int16_t lds_list[];
     const int row = blockIdx.x;
     const int tid = threadIdx.x;
     const int cols = a.cols;
@@ -509,10 +511,16 @@ __global__ __launch_bounds__(256) void reverse_list_kernel(ReverseListArgs a) {
         total += v;
     }
     int pos = before + incl - mine;
-    int16_t* out = a.list + (size_t)row * a.list_pitch;
 #pragma unroll
     for (int k = 0; k < 4; ++k)
-        for (uint32_t x = m[k]; x; x &= x - 1) out[pos++] = (int16_t)((4 * tid + k) * 32 + __ffs(x) - 1);
+        for (uint32_t x = m[k]; x; x &= x - 1) lds_list[pos++] = (int16_t)((4 * tid + k) * 32 + __ffs(x) - 1);
+    __syncthreads();
+    // the first `total` entries out with 16-byte stores (list rows are 16-byte aligned: the
+    // list pitch is a multiple of 8 entries, checked on the host)
+    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+    v4u* dst = (v4u*)(a.list + (size_t)row * a.list_pitch);
+    const v4u* src = (const v4u*)lds_list;
+    for (int i = tid; 8 * i < total; i += 256) dst[i] = src[i];
     if (tid == 0) a.count[row] = total;
 }
 
@@ -915,10 +923,19 @@ hipError_t launch_consistency(const ConsistencyArgs& a, hipStream_t st) {
 hipError_t launch_reverse_list(const ReverseListArgs& a, hipStream_t st) {
     if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
     if (a.cols > 32767 || a.list_pitch < (size_t)a.cols) return hipErrorInvalidValue;
+    if (a.list_pitch % 8 || (uintptr_t)a.list % 16) return hipErrorInvalidValue;
     ReverseListArgs b = a;
     const char* diag = std::getenv("BICOS_REV_LIST_ALL");  // diagnostic: every k-th col1
     b.all = diag ? std::max(1, std::atoi(diag)) : 0;
-    hipLaunchKernelGGL(reverse_list_kernel, dim3(b.rows), dim3(256), 0, st, b);
+    // the LDS list: cols entries, rounded up to whole 16-byte stores
+    const size_t lds = ((size_t)a.cols + 7) / 8 * 16;
+    const auto kern = reverse_list_kernel;
+    if (lds > 64 * 1024 - 4 * 1024 - 64) {
+        const hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, dim3(b.rows), dim3(256), lds, st, b);
     return hipGetLastError();
 }
 
