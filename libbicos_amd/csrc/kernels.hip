@@ -480,10 +480,22 @@ __global__ __launch_bounds__(256) void reverse_list_kernel(ReverseListArgs a) {
     for (int k = 0; k < 4; ++k) mark[tid + 256 * k] = 0u;
     __syncthreads();
     const int16_t* f = a.fwd + (size_t)row * cols;
-    for (int c = tid; c < cols; c += 256) {
-        // (a.all = k > 0: every k-th col1 instead, a timing diagnostic)
-        const int b = a.all ? (c % a.all == 0 ? c : -1) : f[c];
-        if (b >= 0) atomicOr(&mark[b >> 5], 1u << (b & 31));
+    // 8 loads in flight per thread, then their atomics (one load, one atomic at a time took
+    // 18 us at cfg4: 8 dependent global-load latencies per workgroup)
+    for (int base = 0; base < cols; base += 8 * 256) {
+        int v[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int c = base + k * 256 + tid;
+            v[k] = c < cols ? (int)f[c] : -1;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int c = base + k * 256 + tid;
+            // (a.all = k > 0: every k-th col1 instead, a timing diagnostic)
+            const int b = a.all ? (c < cols && c % a.all == 0 ? c : -1) : v[k];
+            if (b >= 0) atomicOr(&mark[b >> 5], 1u << (b & 31));
+        }
     }
     __syncthreads();
     uint32_t m[4];

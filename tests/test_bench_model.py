@@ -68,3 +68,28 @@ def test_key_pair_bound_is_positive_and_ordered():
     nd = bench.mx_key_pair_peak(4, {"variant": 0})
     cons = bench.mx_key_pair_peak(8, {"variant": 1, "no_dupes": False})
     assert 0 < nd < cons
+
+
+def test_scale_model_prediction_rule(tmp_path):
+    """tools/scale_model.py: step = max(rank 0's band x its measured slowdown,
+    one band over one link); N = 1 is the measured whole-frame rate."""
+    import json
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import scale_model
+    recs = [dict(config="cfg2", band_of=8, root_load="none", ms_per_step=0.06),
+            dict(config="cfg2", band_of=8, root_load="proxy16", ms_per_step=0.072),
+            dict(config="cfg2", band_of=8, root_load="dma", ms_per_step=0.0612)]
+    p = tmp_path / "rg.jsonl"
+    p.write_text("\n".join(json.dumps(r) for r in recs))
+    out = scale_model.predict(scale_model.load(str(p)), {"cfg2": 8000.0})
+    by = {(o["gather"], o["link_GBps"]): o for o in out}
+    band_bytes = 192 * 2048 * 6
+    for link in scale_model.LINK_GBPS:
+        t_link = band_bytes / (link * 1e9) * 1e3
+        assert by[("rccl", link)]["predicted_ms_per_step"] == round(max(0.072, t_link), 4)
+        assert by[("dma", link)]["predicted_ms_per_step"] == round(max(0.0612, t_link), 4)
+    o = by[("rccl", 153.0)]
+    assert o["predicted_Mpix_s"] == round(1536 * 2048 / (0.072e-3) / 1e6, 0)
+    assert o["x_vs_N1"] == round(o["predicted_Mpix_s"] / 8000.0, 2)

@@ -1,7 +1,7 @@
 """Regenerate the measured tables of DESIGN.md §8 from the committed bench records:
-profiles/bench_r04.jsonl (the 6 BASELINE configs, then the 20 lines of the reference integration
-grid, with profiles/bench_integ_r04_before.jsonl as the "before" column). The
-tables sit between <!-- BENCH_TABLE --> / <!-- INTEG_TABLE --> markers.
+profiles/bench_r05.jsonl (the 6 BASELINE configs, then the 20 lines of the reference integration
+grid), with profiles/bench_r04.jsonl as the round-4 column. The tables sit between
+<!-- BENCH_TABLE --> / <!-- INTEG_TABLE --> markers.
 
   python tools/design_tables.py
 """
@@ -12,8 +12,15 @@ import re
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 P = os.path.join(ROOT, "profiles")
 
-ROUND3 = {"cfg1": "10712-11885", "cfg2": "7480-7894 (driver 7640)", "cfg3": "3720-3794",
-          "cfg4": "3358-3445", "cfg5": "4931-5001", "readme": "2831-2937"}
+CUR, PREV = "bench_r05.jsonl", "bench_r04.jsonl"
+DRIVER_PREV = {"cfg2": " (driver 7865)"}
+
+
+def bound_text(r):
+    if r["bound"] == "valu":
+        return "%.3f of its key-reduction issue bound (%.3f of dense FP4)" % (
+            r["frac"], r["fp4_view"]["frac"])
+    return "%.3f of dense FP4" % r["frac"]
 
 
 def lines(name):
@@ -25,7 +32,7 @@ def lines(name):
 
 
 def bench_table():
-    L = lines("bench_r04.jsonl")
+    L, P0 = lines(CUR), lines(PREV)
     rows = []
     for c, label in (("cfg1", "cfg1 (8 img, 640×480, 32-bit, nxcorr 0.9)"),
                      ("cfg2", "cfg2 (33 img, 128-bit, nxcorr 0.96) — headline"),
@@ -36,8 +43,10 @@ def bench_table():
         d = L[c]
         r = d["roofline"]
         h = r["hbm"]
-        search = "%.4f ms, %.3f of dense FP4; PMC %.1f MB (algorithmic %.1f)" % (
-            r["ms_per_launch"], r["frac"], r["traffic"] / 1e6, r["algorithmic_bytes"] / 1e6)
+        search = "%.4f ms in frame (%.4f back to back), %s; PMC %s MB (algorithmic %.1f)" % (
+            r["ms_per_launch"], r["back_to_back"]["ms_per_launch"], bound_text(r),
+            "%.1f" % (r["traffic"] / 1e6) if r.get("traffic") else "n/a",
+            r["algorithmic_bytes"] / 1e6)
         if c == "cfg4":
             search += "; %.3f on used bits" % r["used_bits_view"]["frac"]
         if "subpixel" in r:
@@ -47,30 +56,30 @@ def bench_table():
         if c == "readme":
             other += "; one at a time %.3f ms vs ~44 ms on an RTX 4090 (README.md:90): %.1f×" % (
                 d["ms_per_match_one_at_a_time"], d["vs_published"]["speedup"])
-        rows.append("| %s | %.0f | %.4f | %s | %s | %s |" % (label, d["value"], d["ms_per_step"],
-                                                           search, other, ROUND3[c]))
-    head = ["| config | Mpix/s | ms/step | search stage | other stages (back to back) | round 3 Mpix/s |",
+        rows.append("| %s | %.0f | %.4f | %s | %s | %.0f%s |" % (
+            label, d["value"], d["ms_per_step"], search, other, P0[c]["value"], DRIVER_PREV.get(c, "")))
+    head = ["| config | Mpix/s | ms/step | search stage | other stages (back to back) | round 4 Mpix/s |",
             "|---|---|---|---|---|---|"]
     return "\n".join(head + rows)
 
 
 def integ_table():
-    A, B = lines("bench_r04.jsonl"), lines("bench_integ_r04_before.jsonl")
+    A, B = lines(CUR), lines(PREV)
     out = ["| n (bits, set) | one match at a time, ms: no subpixel / 0.25 / 0.20 / 0.15 / 0.10 | "
-           "RTX 4090 ms | × | search ms, frac (executed K / used bits) | first measurement this "
-           "round: ×, search ms |", "|---|---|---|---|---|---|"]
+           "RTX 4090 ms | × | search ms in frame, frac (bound) | round 4: ×, search ms |",
+           "|---|---|---|---|---|---|"]
     for n in (6, 8, 12, 16):
         names = ["integ-n%d" % n] + ["integ-n%d-s%d" % (n, s) for s in (25, 20, 15, 10)]
         d0 = A[names[0]]
         r = d0["roofline"]
         c = d0["config"]
         f = lambda m, k, fmt: fmt % A[m]["vs_published"][k]  # noqa: E731
-        out.append("| %d (%d, %d) | %s | %s | %s | %.3f, %.3f / %.3f | %s, %.3f |" % (
+        out.append("| %d (%d, %d) | %s | %s | %s | %.3f, %.3f (%s) | %s, %.3f |" % (
             n, c["descriptor_bits"], n * n - 2 * n + 3,
             " / ".join(f(m, "ours_ms_one_at_a_time", "%.2f") for m in names),
             " / ".join(f(m, "ms_per_match", "%.1f") for m in names),
             " / ".join(f(m, "speedup", "%.1f") for m in names),
-            r["ms_per_launch"], r["frac"], r["used_bits_view"]["frac"],
+            r["ms_per_launch"], r["frac"], r["bound"],
             " / ".join("%.1f" % B[m]["vs_published"]["speedup"] for m in names),
             B[names[0]]["roofline"]["ms_per_launch"]))
     return "\n".join(out)
