@@ -1074,7 +1074,7 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     cfgname = args.config
     # the search stage's bytes per frame: every search dispatch (tail launches, both
     # Consistency passes, the reverse list) and Consistency's check kernel
-    traffic = load_traffic((kname, "consistency_kernel", "reverse_list_kernel") if cons else kname,
+    traffic = load_traffic((kname, "consistency_kernel") if cons else kname,
                            cfgname, rows)
     # Consistency: the distinct col1 the forward search keeps, over which the reverse search
     # runs (engine.cpp reverse_search)
@@ -1098,9 +1098,9 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
         kview = {"achieved": round(evaluated / t_search / 1e9, 1), "peak": round(kpeak, 1),
                  "unit": "Gpairs/s", "frac": round(evaluated / t_search / 1e9 / kpeak, 4)}
         kname_long = (("search_pk_kernel<%d words> x2 (forward + reverse over the kept col1) + "
-                       "reverse_list_kernel + consistency_kernel" if pk else
+                       "consistency_kernel" if pk else
                        "search_mx_kernel<%d words> x2 (forward + reverse FP4 MFMA Hamming argmin "
-                       "over the kept col1) + reverse_list_kernel + consistency_kernel") % words
+                       "over the kept col1) + consistency_kernel") % words
                       if cons else
                       "search_pk_kernel<%d words> (FP4 MFMA Hamming products, two distances per "
                       "accumulator register, v_pk_minimum3_f16 trees)" % words if pk else

@@ -157,24 +157,17 @@ static int required_bits(int n, int mode) { return mode ? n * n - 2 * n + 3 : 4 
 
 // Consistency's reverse search (reference bicos.hpp:94-106, bicos.cuh:110-135): rev[col1] is
 // read only for the col1 a valid forward match chose, so the matrix-core search runs only
-// over those -- per row the distinct valid fwd[col0] in ascending order (reverse_list_kernel)
-// as compacted col0 entries; rev elsewhere is left unwritten and never read. Periodic
-// inputs whose forward search keeps nothing skip the reverse pass almost entirely.
-// BICOS_REV_FULL=1 (A/B) and the VALU search run the full reverse pass.
-// the reverse list's row pitch: whole 16-byte rows (reverse_list_kernel stores them so)
-static size_t list_pitch(int cols) { return ((size_t)cols + 7) / 8 * 8; }
-
-template <typename F>
-static int reverse_search(bool mx, int rows, int cols, const int16_t* fwd, int16_t* list,
-                          int* count, hipStream_t st, F&& run) {
+// over those -- per row the distinct valid fwd[col0] in ascending order, which each
+// workgroup of the compacted search finds itself (search_mx.hip list_prologue); rev
+// elsewhere is left unwritten and never read. Periodic inputs whose forward search keeps
+// nothing skip the reverse pass almost entirely. BICOS_REV_FULL=1 (A/B) and the VALU search
+// run the full reverse pass. `run(keep)` launches the reverse search, keep = nullptr: full.
+static bool reverse_compacted(bool mx) {
     static const bool full = [] {
         const char* v = std::getenv("BICOS_REV_FULL");
         return v && std::atoi(v) != 0;
     }();
-    if (!mx || full) return run(nullptr, nullptr);
-    bicos_hip::ReverseListArgs la{fwd, list, count, rows, cols, list_pitch(cols)};
-    int rc = check_hip(bicos_hip::launch_reverse_list(la, st), "reverse list launch");
-    return rc ? rc : run(list, count);
+    return mx && !full;
 }
 
 // Bytes the kernels may address from a stack base; the kernels use 32-bit buffer offsets.
@@ -231,15 +224,11 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
 
     const bool mx = use_mx(e);
 
-    // workspace: desc0 | desc1 | raw int16 | fwd | rev | reverse list | list counts
-    // (Consistency)
+    // workspace: desc0 | desc1 | raw int16 | fwd | rev (Consistency)
     const size_t dpitch = bicos_desc_pitch(cols, words);
     const size_t desc_bytes = align_up((size_t)rows * dpitch * 4);
     const size_t map16 = align_up((size_t)rows * cols * 2);
-    const size_t counts = align_up((size_t)rows * 4);
-    const size_t lbytes = align_up((size_t)rows * list_pitch(cols) * 2);
-    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) +
-                  (consistency ? 2 * map16 + lbytes + counts : 0);
+    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) + (consistency ? 2 * map16 : 0);
     int rc = reserve(e->ws, e->ws_bytes, need, e->device, st, e->ws_ready);
     if (rc) return rc;
     // order against earlier users of ws / stage on other streams; mark our use on exit
@@ -259,8 +248,6 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     if (has_nxcorr) p += map16;
     int16_t* fwd = consistency ? (int16_t*)p : nullptr;
     int16_t* rev = consistency ? (int16_t*)(p + map16) : nullptr;
-    int16_t* rlist = consistency ? (int16_t*)(p + 2 * map16) : nullptr;
-    int* rcount = consistency ? (int*)(p + 2 * map16 + lbytes) : nullptr;
 
     // 1. descriptor_transform, both stacks in one launch (cpu.cpp:50-59)
     bicos_hip::TransformArgs ta{s0, s1, d0, d1, n, rows, cols, row_pitch, plane_pitch, dpitch, 0, span};
@@ -271,12 +258,10 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     // forward and the reverse search (the same search with the stacks swapped, bicos.hpp:96)
     // over only the col1 the forward search kept (reverse_search), then the left-right check
     auto search = [&](const uint32_t* a0, const uint32_t* a1, int16_t* out, int out_mode,
-                      bool nd, const char* what, const int16_t* list = nullptr,
-                      const int* lcount = nullptr) {
+                      bool nd, const char* what, const int16_t* keep = nullptr) {
         bicos_hip::SearchArgs sa{a0, a1, out, rows, cols, dpitch, (size_t)cols, out_mode, 0, 0, 0};
-        sa.list = list;
-        sa.lcount = lcount;
-        sa.list_pitch = list_pitch(cols);
+        sa.keep = keep;
+        sa.keep_pitch = (size_t)cols;
         if (mx)
             return check_hip(bicos_hip::launch_search_mx(
                                  sa, mx_geometry(e, rows, cols, words, used_bits(n, mode)), words, nd, st),
@@ -289,9 +274,9 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
         if (rc) return rc;
     } else {
         rc = search(d0, d1, fwd, 1, nodupes, "search launch");
-        if (!rc) rc = reverse_search(mx, rows, cols, fwd, rlist, rcount, st, [&](const int16_t* l, const int* c) {
-            return search(d1, d0, rev, 1, nodupes, "reverse search launch", l, c);
-        });
+        if (!rc)
+            rc = search(d1, d0, rev, 1, nodupes, "reverse search launch",
+                        reverse_compacted(mx) ? fwd : nullptr);
         if (rc) return rc;
         bicos_hip::ConsistencyArgs ca{fwd, rev, raw, rows, cols, (size_t)cols, cfg.max_lr_diff};
         rc = check_hip(bicos_hip::launch_consistency(ca, st), "consistency launch");
@@ -788,9 +773,7 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     if (!e) return fail(BICOS_E_ARG, "consistency search needs an engine workspace");
     std::lock_guard<std::mutex> lk(e->lock);  // the workspace may be shared (default engine)
     const size_t map16 = align_up((size_t)rows * cols * 2);
-    const size_t lbytes = align_up((size_t)rows * list_pitch(cols) * 2);
-    int rc = reserve(e->ws, e->ws_bytes, 2 * map16 + lbytes + align_up((size_t)rows * 4), e->device,
-                     st, e->ws_ready);
+    int rc = reserve(e->ws, e->ws_bytes, 2 * map16, e->device, st, e->ws_ready);
     if (rc) return rc;
     rc = check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent");
     if (rc) return rc;
@@ -801,22 +784,18 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     } mark{e->ws_ready, st};
     int16_t* fwd = (int16_t*)e->ws;
     int16_t* rev = (int16_t*)((char*)e->ws + map16);
-    int16_t* rlist = (int16_t*)((char*)e->ws + 2 * map16);
-    int* rcount = (int*)((char*)e->ws + 2 * map16 + lbytes);
     bicos_hip::SearchArgs fa{desc0, desc1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
     bicos_hip::SearchArgs ra{desc1, desc0, rev, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
     if (mx) {
         const bicos_hip::MxGeometry gm = mx_geometry(e, rows, cols, words, bits);
         rc = check_hip(bicos_hip::launch_search_mx(fa, gm, words, nodupes, st), "search launch");
         if (rc) return rc;
-        rc = reverse_search(true, rows, cols, fwd, rlist, rcount, st,
-                            [&](const int16_t* l, const int* c) {
-                                ra.list = l;
-                                ra.lcount = c;
-                                ra.list_pitch = list_pitch(cols);
-                                return check_hip(bicos_hip::launch_search_mx(ra, gm, words, nodupes, st),
-                                                 "reverse search launch");
-                            });
+        if (reverse_compacted(true)) {
+            ra.keep = fwd;
+            ra.keep_pitch = (size_t)cols;
+        }
+        rc = check_hip(bicos_hip::launch_search_mx(ra, gm, words, nodupes, st),
+                       "reverse search launch");
     } else {
         rc = check_hip(bicos_hip::launch_search(fa, g, words, nodupes, st), "search launch");
         if (rc) return rc;

@@ -461,81 +461,6 @@ __global__ __launch_bounds__(256) void consistency_kernel(ConsistencyArgs a) {
     a.out[(size_t)row * a.out_pitch + col] = v;
 }
 
-// Consistency's reverse-search set (reference bicos.hpp:94-101 and bicos.cuh:114,124-131: the
-// reverse search runs only where the forward one found a valid match): one 256-thread
-// workgroup per row marks the col1 some forward match chose in an LDS bitmap (<= 1024 words:
-// cols <= 32767), then each thread takes 4 consecutive words -- an exclusive scan of their
-// popcounts gives its first list slot -- and writes their marked col1 in ascending order into
-// an LDS copy of the list (dynamic, cols x 2 bytes), which the workgroup stores with 16-byte
-// writes. (Scattered 2-byte global stores, one per marked column, took 23.7 us at cfg4:
-// every store instruction touched ~64 cache lines.)
-__global__ __launch_bounds__(256) void reverse_list_kernel(ReverseListArgs a) {
-    __shared__ uint32_t mark[1024];
-    __shared__ int wsum[4];
-    extern __shared__ __attribute__((aligned(16))) int16_t lds_list[];
-    const int row = blockIdx.x;
-    const int tid = threadIdx.x;
-    const int cols = a.cols;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) mark[tid + 256 * k] = 0u;
-    __syncthreads();
-    const int16_t* f = a.fwd + (size_t)row * cols;
-    // 8 loads in flight per thread, then their atomics (one load, one atomic at a time took
-    // 18 us at cfg4: 8 dependent global-load latencies per workgroup)
-    for (int base = 0; base < cols; base += 8 * 256) {
-        int v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int c = base + k * 256 + tid;
-            v[k] = c < cols ? (int)f[c] : -1;
-        }
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int c = base + k * 256 + tid;
-            // (a.all = k > 0: every k-th col1 instead, a timing diagnostic)
-            const int b = a.all ? (c < cols && c % a.all == 0 ? c : -1) : v[k];
-            if (b >= 0) atomicOr(&mark[b >> 5], 1u << (b & 31));
-        }
-    }
-    __syncthreads();
-    uint32_t m[4];
-    int mine = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        m[k] = mark[4 * tid + k];  // (words past cols / 32 are 0)
-        mine += __popc(m[k]);
-    }
-    // inclusive scan of the per-thread counts within the wave, then across the 4 waves
-    const int lane = tid & 63, wave = tid >> 6;
-    int incl = mine;
-#pragma unroll
-    for (int s = 1; s < 64; s <<= 1) {
-        const int y = __shfl_up(incl, s);
-        if (lane >= s) incl += y;
-    }
-    if (lane == 63) wsum[wave] = incl;
-    __syncthreads();
-    int before = 0, total = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        const int v = wsum[w];
-        before += w < wave ? v : 0;
-        total += v;
-    }
-    int pos = before + incl - mine;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-        for (uint32_t x = m[k]; x; x &= x - 1) lds_list[pos++] = (int16_t)((4 * tid + k) * 32 + __ffs(x) - 1);
-    __syncthreads();
-    // the first `total` entries out with 16-byte stores (list rows are 16-byte aligned: the
-    // list pitch is a multiple of 8 entries, checked on the host)
-    typedef uint32_t v4u __attribute__((ext_vector_type(4)));
-    v4u* dst = (v4u*)(a.list + (size_t)row * a.list_pitch);
-    const v4u* src = (const v4u*)lds_list;
-    for (int i = tid; 8 * i < total; i += 256) dst[i] = src[i];
-    if (tid == 0) a.count[row] = total;
-}
-
 // ---------------------------------------------------------------------- agree
 
 // fma_p / div_p / sqrt_p (IEEE, correctly rounded): nxc.hpp
@@ -929,25 +854,6 @@ hipError_t launch_consistency(const ConsistencyArgs& a, hipStream_t st) {
     if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
     dim3 grid((a.cols + 255) / 256, a.rows);
     hipLaunchKernelGGL(consistency_kernel, grid, dim3(256), 0, st, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_reverse_list(const ReverseListArgs& a, hipStream_t st) {
-    if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
-    if (a.cols > 32767 || a.list_pitch < (size_t)a.cols) return hipErrorInvalidValue;
-    if (a.list_pitch % 8 || (uintptr_t)a.list % 16) return hipErrorInvalidValue;
-    ReverseListArgs b = a;
-    const char* diag = std::getenv("BICOS_REV_LIST_ALL");  // diagnostic: every k-th col1
-    b.all = diag ? std::max(1, std::atoi(diag)) : 0;
-    // the LDS list: cols entries, rounded up to whole 16-byte stores
-    const size_t lds = ((size_t)a.cols + 7) / 8 * 16;
-    const auto kern = reverse_list_kernel;
-    if (lds > 64 * 1024 - 4 * 1024 - 64) {
-        const hipError_t e = hipFuncSetAttribute((const void*)kern,
-                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(kern, dim3(b.rows), dim3(256), lds, st, b);
     return hipGetLastError();
 }
 

@@ -35,25 +35,12 @@ struct SearchArgs {
     int tail_col0;          // set by launch_search_mx: first col0 of the tail workgroups
     int tail_T;             // set by launch_search_mx: their tiles per wave (0: no tail)
     // Compacted col0 (launch_search_mx only; nullptr: every col0 of the row). Row r matches
-    // only the lcount[r] col0 list[r * list_pitch + i], i < lcount[r], writing out[list[..]]:
-    // Consistency's reverse search over the col1 the forward search kept (make_reverse_list)
-    const int16_t* list;
-    const int* lcount;
-    size_t list_pitch;      // int16 elements
+    // only the distinct col1 >= 0 of keep[r * keep_pitch + c], c < cols, in ascending order,
+    // writing out[col]: Consistency's reverse search over the col1 its forward search kept
+    // (keep = the forward result, best col1 or -1; reference bicos.hpp:94-101)
+    const int16_t* keep;
+    size_t keep_pitch;      // int16 elements
 };
-
-// Per row, the distinct col1 >= 0 of fwd (a forward search's best col1, -1 = invalid) in
-// ascending order, and their count (reference bicos.hpp:94-101: the reverse search runs only
-// for pixels whose forward search was valid)
-struct ReverseListArgs {
-    const int16_t* fwd;     // [rows][cols]
-    int16_t* list;          // [rows][list_pitch]
-    int* count;             // [rows]
-    int rows, cols;
-    size_t list_pitch;
-    int all;                // set by launch_reverse_list (BICOS_REV_LIST_ALL=k: every k-th col1)
-};
-hipError_t launch_reverse_list(const ReverseListArgs& a, hipStream_t st);
 
 struct SearchGeometry {
     int chunk;              // col1 columns per LDS fill

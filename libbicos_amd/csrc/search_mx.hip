@@ -205,11 +205,16 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 // A workgroup scans one row for the col0 range [c0_base + tile * waves * T * 32, + waves * T *
 // 32), c0_base = a.tail_col0 for the tail launch (launch_mx), else 0.
 //
-// LIST: the col0 of row r are the lcount[r] compacted entries list[r][i] (Consistency's
-// reverse search over the col1 its forward search kept, see make_reverse_list in engine.cpp);
-// the index ranges above run over i, workgroups past the row's count exit at once, and the
-// block order starts REV_AHEAD columns above the wave's highest entry (a reverse match lies
-// at col0 = col1 + d, d >= 0 in a rectified pair).
+// LIST: the col0 of row r are the distinct col1 >= 0 of row r of a.keep (Consistency's reverse
+// search over the col1 its forward search kept, engine.cpp reverse_search), in ascending
+// order: entry i is the i-th of them. The workgroup finds its own entries in a prologue
+// (list_prologue); the index ranges above run over i, workgroups past the row's count exit,
+// and the block order starts REV_AHEAD columns above the wave's highest entry (a reverse
+// match lies at col0 = col1 + d, d >= 0 in a rectified pair). The tail split is the full
+// search's, in entry space: the main launch takes entries below tail_col0, the tail launch
+// the rest (a dense row then costs what it does uncompacted: without the tail, the 4th
+// workgroup of a 3300-column row ran 228 entries for a whole-row scan, planted stereo
+// NODUPES|CONSISTENCY 2.38 vs 2.24 ms).
 // (row, tile) of a compacted (LIST) launch: grid = 8 x ceil(R8 / G) G x tiles_per_row, R8 =
 // ceil(rows / 8), G = LIST_GROUP rows. XCD x = bid % 8 owns rows [x R8, (x + 1) R8), and
 // within the XCD the order is tile-major per group of G rows: the group's tile 0 workgroups,
@@ -222,6 +227,119 @@ __device__ __forceinline__ int key_col(uint32_t key) {
 // XCD holds at once (32 CUs x 2 workgroups), so a row's workgroups run together again.
 // Rows past the XCD's range (or past rows) exit.
 constexpr int LIST_GROUP = 32;
+
+// LIST prologue scratch at the start of the dynamic LDS (before the first chunk is staged):
+// the row's kept-column bitmap (<= 1024 words: cols <= 32767) and 8 wave sums; the
+// workgroup's entry columns live after the chunk region
+constexpr int LIST_SCRATCH_BYTES = (1024 + 8) * 4;
+static_assert(LIST_SCRATCH_BYTES % 16 == 0, "scratch size");
+
+// Consistency's compacted reverse search, the reference's rule (bicos.hpp:94-101,
+// bicos.cuh:114,124-131: the reverse search runs only where the forward one found a valid
+// match), computed by each workgroup for its own row: the distinct col1 >= 0 of the forward
+// result `f` (cols entries) marked in an LDS bitmap, a scan of the words' popcounts, and the
+// columns of entries [e0, e0 + ne) written into `ent` by the threads owning their words. Returns the row's entry count (workgroup-uniform). Every
+// thread of the workgroup must call it (barriers). Round 5 ran this as a separate kernel
+// writing a list to HBM first: 18 us per cfg4 frame; here it overlaps the other resident
+// workgroup's matrix-core work.
+__device__ int list_prologue(const int16_t* __restrict__ f, int cols, uint32_t* scratch,
+                             int16_t* ent, int e0, int ne) {
+    const int tid = threadIdx.x, bs = blockDim.x;
+    const int nw = (cols + 31) >> 5;
+    uint32_t* bits = scratch;
+    int* wsum = (int*)(scratch + 1024);
+    for (int w = tid; w < nw; w += bs) bits[w] = 0u;
+    for (int i = tid; i < ne; i += bs) ent[i] = 0;  // entries past the row's count
+    __syncthreads();
+    // mark: 8 forward results per thread and 16-byte load where the row is aligned (it is
+    // when cols % 8 == 0); a run of results in one bitmap word is one LDS atomic (a stereo
+    // row's col1 ascend with col0, so most threads issue one or two)
+    auto mark8 = [&](const int (&v)[8]) {
+        int cw = -1;
+        uint32_t m = 0u;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (v[k] < 0) continue;
+            const int w = v[k] >> 5;
+            if (w != cw) {
+                if (cw >= 0) atomicOr(&bits[cw], m);
+                cw = w;
+                m = 0u;
+            }
+            m |= 1u << (v[k] & 31);
+        }
+        if (cw >= 0) atomicOr(&bits[cw], m);
+    };
+    if ((reinterpret_cast<uintptr_t>(f) & 15u) == 0) {
+        for (int c = 8 * tid; c < cols; c += 8 * bs) {
+            int v[8];
+            if (c + 8 <= cols) {
+                const v4i x = *reinterpret_cast<const v4i*>(f + c);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    v[2 * k] = (int)(int16_t)(x[k] & 0xFFFF);
+                    v[2 * k + 1] = (int)(int16_t)((uint32_t)x[k] >> 16);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) v[k] = c + k < cols ? (int)f[c + k] : -1;
+            }
+            mark8(v);
+        }
+    } else {
+        for (int c = 8 * tid; c < cols; c += 8 * bs) {
+            int v[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) v[k] = c + k < cols ? (int)f[c + k] : -1;
+            mark8(v);
+        }
+    }
+    __syncthreads();
+    // thread t owns words [t q, t q + q): popcounts, a wave scan and the wave sums give its
+    // first entry index; it writes the columns of its set bits that fall in [e0, e0 + ne)
+    const int q = (nw + bs - 1) / bs;
+    int mine = 0;
+    for (int k = 0; k < q; ++k) {
+        const int w = tid * q + k;
+        mine += w < nw ? __popc(bits[w]) : 0;
+    }
+    const int lane = tid & 63, wave = tid >> 6, nwaves = bs >> 6;
+    int incl = mine;
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+        const int y = __shfl_up(incl, sh);
+        if (lane >= sh) incl += y;
+    }
+    if (lane == 63) wsum[wave] = incl;
+    __syncthreads();
+    int before = 0, total = 0;
+    for (int w = 0; w < nwaves; ++w) {
+        const int v = wsum[w];
+        before += w < wave ? v : 0;
+        total += v;
+    }
+    int e = before + incl - mine;
+    if (e < e0 + ne && e + mine > e0) {
+        for (int k = 0; k < q; ++k) {
+            const int w = tid * q + k;
+            uint32_t x = w < nw ? bits[w] : 0u;
+            while (x) {
+                const int b = __builtin_ctz(x);
+                x &= x - 1u;
+                if (e >= e0 && e < e0 + ne) ent[e - e0] = (int16_t)(32 * w + b);
+                ++e;
+            }
+        }
+    }
+    __syncthreads();
+    return __builtin_amdgcn_readfirstlane(total);
+}
+
+// byte offset of the LIST entry columns in the dynamic LDS: past the chunk region and the
+// prologue scratch
+__host__ __device__ inline int list_ent_offset(int chunk_bytes) {
+    return chunk_bytes > LIST_SCRATCH_BYTES ? (chunk_bytes + 15) / 16 * 16 : LIST_SCRATCH_BYTES;
+}
 __device__ __forceinline__ void list_row_tile(int tiles_per_row, int rows, int& row, int& tile) {
     const int r8 = (rows + 7) / 8;
     const int j = blockIdx.x / 8;
@@ -236,11 +354,23 @@ inline int list_grid(int rows, int tiles_per_row) {
     return 8 * ((r8 + LIST_GROUP - 1) / LIST_GROUP) * LIST_GROUP * tiles_per_row;
 }
 
-constexpr int REV_AHEAD = 64;
+// LIST block order: a wave's blocks start REV_AHEAD columns above its highest entry, a
+// workgroup's chunks at the chunk of its highest entry (REV_AHEAD_CHUNK = 0). Starting the
+// chunks 64 columns up as well sent every wave through the chunk above first, where only the
+// top few entries have their matches: dense rows (planted / low-texture NODUPES|CONSISTENCY
+// at 3300 columns) 2.37 / 2.38 ms vs 2.30 / 2.25 (REV_AHEAD 0 / 32: planted 2.35 / 2.32;
+// profiles/reverse_search_r05.jsonl)
+#ifndef BICOS_REV_AHEAD
+#define BICOS_REV_AHEAD 64
+#endif
+#ifndef BICOS_REV_AHEAD_CHUNK
+#define BICOS_REV_AHEAD_CHUNK 0
+#endif
+constexpr int REV_AHEAD = BICOS_REV_AHEAD;
+constexpr int REV_AHEAD_CHUNK = BICOS_REV_AHEAD_CHUNK;
 template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIST>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KSU >= 4 ? 3 : 4)))
 void search_mx_kernel(SearchArgs a) {
-    static_assert(!(TAIL && LIST), "compacted searches have no tail launch");
     constexpr bool FK = KEYS == 3;
     static_assert(!FK || !NODUPES, "FK keys: first minimum only");
     constexpr bool XK = KEYS == 1 || KEYS == 2;
@@ -279,14 +409,23 @@ void search_mx_kernel(SearchArgs a) {
     const int chunk = a.chunk;
     const int waves = blockDim.x >> 6;
     const int c0_wave = c0_base + (tile * waves + wave) * (T * 32);
-    // col0 entries of this row (LIST: the compacted count; workgroup-uniform)
-    const int lcols = LIST ? __builtin_amdgcn_readfirstlane(a.lcount[row]) : cols;
-    const int16_t* __restrict__ lrow = LIST ? a.list + (size_t)row * a.list_pitch : nullptr;
-    if (LIST && tile * waves * T * 32 >= lcols) return;  // the whole workgroup: no barrier yet
+    // col0 entries of this row (LIST: the compacted count, found by the prologue; the
+    // workgroup's entry columns in LDS past the chunk region)
+    int lcols = cols;
+    const int e0 = c0_base + tile * waves * T * 32;
+    int16_t* ent = nullptr;
+    if constexpr (LIST) {
+        constexpr int WLL = 2 * KSU;
+        ent = (int16_t*)((char*)lds_mx + list_ent_offset(WLL * chunk * 16));
+        lcols = list_prologue(a.keep + (size_t)row * a.keep_pitch, cols, (uint32_t*)lds_mx, ent,
+                              e0, waves * T * 32);
+        if (!TAIL) lcols = min(lcols, a.tail_col0);  // the tail launch takes the entries past it
+        if (e0 >= lcols) return;  // the whole workgroup, past the prologue's barriers
+    }
     // LIST: the column of entry i (ascending in i); the block order's start for entries < e
-    auto lcol = [&](int i) { return LIST ? (int)lrow[i] : i; };
-    auto start_col = [&](int e) {
-        return LIST ? min(cols - 1, (int)lrow[min(e, lcols) - 1] + REV_AHEAD) : min(cols - 1, e - 1);
+    auto lcol = [&](int i) { return LIST ? (int)ent[i - e0] : i; };
+    auto start_col = [&](int e, int ahead) {
+        return LIST ? min(cols - 1, (int)ent[min(e, lcols) - 1 - e0] + ahead) : min(cols - 1, e - 1);
     };
 
     const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
@@ -445,7 +584,7 @@ void search_mx_kernel(SearchArgs a) {
     const int nchunks = (cols + chunk - 1) / chunk;
     // FREE: chunks downwards from the one holding the workgroup's highest col0
     int cstart = 0;
-    if constexpr (FREE) cstart = start_col(c0_base + (tile + 1) * waves * T * 32) / chunk;
+    if constexpr (FREE) cstart = start_col(c0_base + (tile + 1) * waves * T * 32, REV_AHEAD_CHUNK) / chunk;
     for (int k = 0; k < nchunks; ++k) {
         int ci = FREE ? cstart - k : k;
         if (ci < 0) ci += nchunks;
@@ -567,7 +706,7 @@ void search_mx_kernel(SearchArgs a) {
         if constexpr (FREE) {
             if (partial) partial_block(cc);
             // full blocks downwards from the one holding the wave's highest col0 (clamped)
-            const int sb = max(0, min(nfull - 1, (start_col(c0_wave + 32 * T) - base) / 32));
+            const int sb = max(0, min(nfull - 1, (start_col(c0_wave + 32 * T, REV_AHEAD) - base) / 32));
 #if !defined(BICOS_MX_DIAG) || BICOS_MX_DIAG >= 3
             if constexpr (PIPE) {
                 // software pipeline over the blocks (one tile pair per wave): the products of
@@ -804,7 +943,6 @@ template <int WORDS, int T, bool TAIL, bool LIST>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void search_pk_kernel(SearchArgs a) {
     static_assert(T == 1 || T % 2 == 0, "wide tiles: 1 or pairs");
-    static_assert(!(TAIL && LIST), "compacted searches have no tail launch");
     constexpr int NP = T == 1 ? 1 : T / 2;
     extern __shared__ __attribute__((aligned(16))) v4i lds_mx[];  // [WORDS][chunk]
 
@@ -829,12 +967,19 @@ void search_pk_kernel(SearchArgs a) {
     const int waves = blockDim.x >> 6;
     const int c0_base = TAIL ? a.tail_col0 : 0;
     const int c0_wave = c0_base + (tile * waves + wave) * (T * 64);
-    const int lcols = LIST ? __builtin_amdgcn_readfirstlane(a.lcount[row]) : cols;
-    const int16_t* __restrict__ lrow = LIST ? a.list + (size_t)row * a.list_pitch : nullptr;
-    if (LIST && tile * waves * T * 64 >= lcols) return;  // the whole workgroup: no barrier yet
-    auto lcol = [&](int i) { return LIST ? (int)lrow[i] : i; };
-    auto start_col = [&](int e) {
-        return LIST ? min(cols - 1, (int)lrow[min(e, lcols) - 1] + REV_AHEAD) : min(cols - 1, e - 1);
+    int lcols = cols;
+    const int e0 = c0_base + tile * waves * T * 64;
+    int16_t* ent = nullptr;
+    if constexpr (LIST) {
+        ent = (int16_t*)((char*)lds_mx + list_ent_offset(WORDS * chunk * 16));
+        lcols = list_prologue(a.keep + (size_t)row * a.keep_pitch, cols, (uint32_t*)lds_mx, ent,
+                              e0, waves * T * 64);
+        if (!TAIL) lcols = min(lcols, a.tail_col0);  // the tail launch takes the entries past it
+        if (e0 >= lcols) return;  // the whole workgroup, past the prologue's barriers
+    }
+    auto lcol = [&](int i) { return LIST ? (int)ent[i - e0] : i; };
+    auto start_col = [&](int e, int ahead) {
+        return LIST ? min(cols - 1, (int)ent[min(e, lcols) - 1 - e0] + ahead) : min(cols - 1, e - 1);
     };
 
     const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
@@ -925,7 +1070,7 @@ void search_pk_kernel(SearchArgs a) {
     // chunks downwards from the one holding the workgroup's highest col0, blocks downwards
     // from the wave's highest col0 (stereo matches lie at col1 <= col0 within a few blocks,
     // so the running minimum is found early and later blocks rarely take the branch)
-    const int cstart = start_col(c0_base + (tile + 1) * waves * T * 64) / chunk;
+    const int cstart = start_col(c0_base + (tile + 1) * waves * T * 64, REV_AHEAD_CHUNK) / chunk;
     for (int k = 0; k < nchunks; ++k) {
         int ci = cstart - k;
         if (ci < 0) ci += nchunks;
@@ -976,7 +1121,7 @@ void search_pk_kernel(SearchArgs a) {
             }
         };
         if ((ncols & 31) != 0) block(nfull, true);
-        const int sb0 = max(0, min(nfull - 1, (start_col(c0_wave + 64 * T) - base) / 32));
+        const int sb0 = max(0, min(nfull - 1, (start_col(c0_wave + 64 * T, REV_AHEAD) - base) / 32));
         for (int i = 0; i < nfull; ++i) {
             int b = sb0 - i;
             if (b < 0) b += nfull;
@@ -1012,7 +1157,8 @@ void search_pk_kernel(SearchArgs a) {
 
 template <int WORDS, int T, bool TAIL, bool LIST = false>
 hipError_t launch_pk_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st) {
-    const size_t lds = (size_t)WORDS * a.chunk * 16;
+    size_t lds = (size_t)WORDS * a.chunk * 16;
+    if (LIST) lds = list_ent_offset((int)lds) + (size_t)waves * T * 64 * 2;
     const auto kern = search_pk_kernel<WORDS, T, TAIL, LIST>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -1041,20 +1187,21 @@ inline void tail_shape(SearchArgs& t, int& waves, int cols_per_wave) {
 
 // main launch over [0, tail_col0); the tail (one workgroup per row, one wide tile per wave)
 // over [tail_col0, cols) when the geometry asked for one (see launch_mx_tt)
+// (compacted col0, a.keep: the same split in entry space -- the main workgroups take the
+// row's entries below tail_col0, those past the row's count exit; the tail workgroup the
+// entries from tail_col0 on, if the row has any)
 template <int WORDS, int T>
 hipError_t launch_pk(const SearchArgs& a, int waves, hipStream_t st) {
-    if (a.list) {  // compacted col0: workgroups for the whole width, those past the count exit
-        SearchArgs b = a;
-        b.tiles_per_row = (int)((a.cols + 64L * waves * T - 1) / (64L * waves * T));
-        return launch_pk_grid<WORDS, T, false, true>(b, waves, list_grid(a.rows, b.tiles_per_row), st);
-    }
-    hipError_t e = launch_pk_grid<WORDS, T, false>(a, waves, a.rows * a.tiles_per_row, st);
+    const bool list = a.keep != nullptr;
+    hipError_t e = list ? launch_pk_grid<WORDS, T, false, true>(a, waves, list_grid(a.rows, a.tiles_per_row), st)
+                        : launch_pk_grid<WORDS, T, false>(a, waves, a.rows * a.tiles_per_row, st);
     if constexpr (T > 1) {
         if (e == hipSuccess && a.tail_col0 < a.cols) {
             SearchArgs t = a;
             int tw = waves;
             tail_shape(t, tw, 64);
-            e = launch_pk_grid<WORDS, 1, true>(t, tw, a.rows, st);
+            e = list ? launch_pk_grid<WORDS, 1, true, true>(t, tw, list_grid(a.rows, 1), st)
+                     : launch_pk_grid<WORDS, 1, true>(t, tw, a.rows, st);
         }
     }
     return e;
@@ -1074,7 +1221,8 @@ hipError_t launch_pk_w(const SearchArgs& a, const MxGeometry& g, hipStream_t st)
 template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIST = false>
 hipError_t launch_mx_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st) {
     constexpr int WL = 2 * KSU;
-    const size_t lds = (size_t)WL * a.chunk * 16;
+    size_t lds = (size_t)WL * a.chunk * 16;
+    if (LIST) lds = list_ent_offset((int)lds) + (size_t)waves * T * 32 * 2;
     const auto kern = search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, TAIL, LIST>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
@@ -1092,9 +1240,13 @@ hipError_t launch_mx_grid(const SearchArgs& a, int waves, int nwg, hipStream_t s
 // T-tile scan: 3208 columns are 3 x 1024 + 136, and the 4th workgroup of every row ran 2 of its
 // 8 waves for a full-length scan. (One heterogeneous launch would also fill the main launch's
 // last round, but hosting both tile counts in one kernel made the main path spill.)
+// Compacted col0 (a.keep) split the same way in entry space (see launch_pk).
 template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, int TT>
 hipError_t launch_mx_tt(const SearchArgs& a, int waves, hipStream_t st) {
-    hipError_t e = launch_mx_grid<WORDS, KSU, NODUPES, T, KEYS, false>(a, waves, a.rows * a.tiles_per_row, st);
+    const bool list = a.keep != nullptr;
+    hipError_t e = list ? launch_mx_grid<WORDS, KSU, NODUPES, T, KEYS, false, true>(
+                              a, waves, list_grid(a.rows, a.tiles_per_row), st)
+                        : launch_mx_grid<WORDS, KSU, NODUPES, T, KEYS, false>(a, waves, a.rows * a.tiles_per_row, st);
     if constexpr (TT == 0) {
         return e;
     } else {
@@ -1102,7 +1254,8 @@ hipError_t launch_mx_tt(const SearchArgs& a, int waves, hipStream_t st) {
         SearchArgs t = a;
         int tw = waves;
         tail_shape(t, tw, 32 * TT);
-        return launch_mx_grid<WORDS, KSU, NODUPES, TT, KEYS, true>(t, tw, a.rows, st);
+        return list ? launch_mx_grid<WORDS, KSU, NODUPES, TT, KEYS, true, true>(t, tw, list_grid(a.rows, 1), st)
+                    : launch_mx_grid<WORDS, KSU, NODUPES, TT, KEYS, true>(t, tw, a.rows, st);
     }
 }
 
@@ -1111,10 +1264,10 @@ hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     // (tail tiles: 1 or 2, and fewer than the main workgroups'; KEYS 2 only -- the any-order
     // NoDuplicates search, whose block order starts at each wave's own col0)
     if constexpr (KEYS == 2 && T >= 2) {
-        if (!a.list && a.tail_T == 1 && a.tail_col0 < a.cols) return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 1>(a, waves, st);
+        if (a.tail_T == 1 && a.tail_col0 < a.cols) return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 1>(a, waves, st);
     }
     if constexpr (KEYS == 2 && T >= 4) {
-        if (!a.list && a.tail_T == 2 && a.tail_col0 < a.cols) return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 2>(a, waves, st);
+        if (a.tail_T == 2 && a.tail_col0 < a.cols) return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 2>(a, waves, st);
     }
     // no tail workgroups for these keys / tile counts: the main workgroups cover every col0
     SearchArgs b = a;
@@ -1122,9 +1275,6 @@ hipError_t launch_mx(const SearchArgs& a, int waves, hipStream_t st) {
     b.tiles_per_row = (int)((a.cols + per_wg - 1) / per_wg);
     b.tail_T = 0;
     b.tail_col0 = a.cols;
-    if (a.list)  // compacted col0: the workgroups past a row's count exit at once
-        return launch_mx_grid<WORDS, KSU, NODUPES, T, KEYS, false, true>(
-            b, waves, list_grid(a.rows, b.tiles_per_row), st);
     return launch_mx_tt<WORDS, KSU, NODUPES, T, KEYS, 0>(b, waves, st);
 }
 

@@ -189,17 +189,10 @@ for step in "$@"; do
                     run rl_${c}_${m}$k 300 python bench.py --config $c --band-of ${RLN:-8} --inflight 3 --steps 400 --warmup 10 --no-cpu-baseline --no-host-path --kernel-reps 0 $extra
                 done
             done; done ;;
-        revprof)  # kernel trace of the random-descriptor searches: kept col1 / full reverse / every col1 through the list
+        revprof)  # kernel trace of the random-descriptor searches: kept col1 / full reverse
             run revprof_kept 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof_kept -o run --output-format csv -- python tools/random_search_bench.py --words 4 --inputs random_u128 --reps 5
-            BICOS_REV_FULL=1 run revprof_full 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof_full -o run --output-format csv -- python tools/random_search_bench.py --words 4 --inputs random_u128 --reps 5
-            BICOS_REV_LIST_ALL=1 run revprof_all 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof_all -o run --output-format csv -- python tools/random_search_bench.py --words 4 --inputs random_u128 --reps 5 ;;
+            BICOS_REV_FULL=1 run revprof_full 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof_full -o run --output-format csv -- python tools/random_search_bench.py --words 4 --inputs random_u128 --reps 5 ;;
         hostdma) run hostdma 300 python tools/host_dma_probe.py ;;
-        hostab)  # band-wise downloads (default) vs one download at the end (BICOS_HOST_DL=0), interleaved twice
-            for k in 1 2; do
-                run hostab_band$k 300 python tools/host_bench.py --reps 7
-                BICOS_HOST_DL=0 run hostab_end$k 300 python tools/host_bench.py --reps 7
-            done
-            BICOS_HOST_TRACE=1 run hostab_trace 300 python tools/host_bench.py --reps 2 ;;
         revrand)  # random-descriptor searches (32/64/128-bit) with the compacted reverse search vs the full one
             run revrand_kept 600 python tools/random_search_bench.py --words 1,2,4 --out gpurun_out/random_search_kept.jsonl
             BICOS_REV_FULL=1 run revrand_full 600 python tools/random_search_bench.py --words 1,2,4 --out gpurun_out/random_search_full.jsonl
@@ -207,14 +200,9 @@ for step in "$@"; do
                 run bench4_kept$k 300 python bench.py --config cfg4 --steps 20 --warmup 3 --no-cpu-baseline --no-host-path
                 BICOS_REV_FULL=1 run bench4_full$k 300 python bench.py --config cfg4 --steps 20 --warmup 3 --no-cpu-baseline --no-host-path
             done ;;
-        revstride)  # the compacted reverse search over every k-th col1 (timing diagnostic), kernel trace
-            for k in 1 2 4 8; do
-                BICOS_REV_LIST_ALL=$k run revstride_$k 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revstride_$k -o run --output-format csv -- python tools/random_search_bench.py --words 4 --inputs random_u128 --reps 3
-            done ;;
-        revprof4)  # cfg4 kernel stats one frame at a time: compacted reverse, full reverse, every col1 through the list
+        revprof4)  # cfg4 kernel stats one frame at a time: compacted reverse, full reverse
             run revprof4_kept 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof4_kept -o run --output-format csv -- python bench.py --config cfg4 --steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --no-host-path --kernel-reps 0
-            BICOS_REV_FULL=1 run revprof4_full 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof4_full -o run --output-format csv -- python bench.py --config cfg4 --steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --no-host-path --kernel-reps 0
-            BICOS_REV_LIST_ALL=1 run revprof4_all 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof4_all -o run --output-format csv -- python bench.py --config cfg4 --steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --no-host-path --kernel-reps 0 ;;
+            BICOS_REV_FULL=1 run revprof4_full 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof4_full -o run --output-format csv -- python bench.py --config cfg4 --steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --no-host-path --kernel-reps 0 ;;
         revab)  # Consistency's reverse search over the kept col1 vs the full reverse pass (BICOS_REV_FULL=1)
             run randsearch_kept 600 python tools/random_search_bench.py --words 1,2,4 --out gpurun_out/random_search_kept.jsonl
             BICOS_REV_FULL=1 run randsearch_full 600 python tools/random_search_bench.py --words 1,2,4 --out gpurun_out/random_search_full.jsonl
