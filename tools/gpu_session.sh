@@ -193,6 +193,15 @@ for step in "$@"; do
             run revprof_kept 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof_kept -o run --output-format csv -- python tools/random_search_bench.py --words 4 --inputs random_u128 --reps 5
             BICOS_REV_FULL=1 run revprof_full 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof_full -o run --output-format csv -- python tools/random_search_bench.py --words 4 --inputs random_u128 --reps 5 ;;
         hostdma) run hostdma 300 python tools/host_dma_probe.py ;;
+        swband)  # search geometries for row bands (cfg2 N = 8 / 4 bands and the whole frame), back to back
+            for r in ${ROWS:-192 384 1536}; do
+                run swband_$r 300 python tools/search_sweep.py --config ${SC:-cfg2} --rows $r --rounds 7 --reps 10 \
+                    --variants "${VARS:-0:0:0,64:2:8:0,64:4:8:0,64:2:8:40,64:2:8:48,64:4:8:48,64:2:4:32,64:4:4:32,64:4:4:0}"
+            done ;;
+        bandprof)  # kernel stats of band 0 of a BAND-way split (default cfg2 / 8), one frame at a time and 3 in flight
+            for f in 1 3; do
+                run bandprof_${SC:-cfg2}_${BAND:-8}_f$f 300 rocprofv3 --kernel-trace --stats -d gpurun_out/bandprof_${SC:-cfg2}_${BAND:-8}_f$f -o run --output-format csv -- python bench.py --config ${SC:-cfg2} --band-of ${BAND:-8} --steps 100 --warmup 5 --inflight $f --no-cpu-baseline --no-host-path --kernel-reps 0
+            done ;;
         revrand)  # random-descriptor searches (32/64/128-bit) with the compacted reverse search vs the full one
             run revrand_kept 600 python tools/random_search_bench.py --words 1,2,4 --out gpurun_out/random_search_kept.jsonl
             BICOS_REV_FULL=1 run revrand_full 600 python tools/random_search_bench.py --words 1,2,4 --out gpurun_out/random_search_full.jsonl
