@@ -11,7 +11,7 @@ to rank 0 with ONE RCCL gather per step, inside the timed region; the gather of
 step k overlaps the kernels of step k+1 (double-buffered), and every gather has
 completed before the closing barrier.
 
-Frames in flight (--inflight F; default 2 for one GPU, 3 for row bands on N > 1): step k
+Frames in flight (--inflight F; default 2 for one GPU, 6 for row bands on N > 1): step k
 runs on stream k % F with its own
 engine and output buffers, so consecutive frames overlap the way a camera stream is
 processed -- the HBM-bound transform / agree of one frame fill the compute-unit slots the
@@ -325,9 +325,9 @@ def main():
                          "one frame's HBM-bound stages fill the slots the previous frame's "
                          "search leaves idle (1 = strictly one match after another). Default: "
                          "2 on one GPU (whole frames: cfg2 7701-7771 vs 7535-7576 Mpix/s with "
-                         "3, cfg1 11642-11979 vs 7076-9867; profiles/inflight_r02.jsonl), 3 for "
-                         "N > 1 row bands (N=8 band 0.0548 vs 0.0577 ms with 2; "
-                         "profiles/frame_pipe_r02.jsonl)")
+                         "3, cfg1 11642-11979 vs 7076-9867; profiles/inflight_r02.jsonl), 6 for "
+                         "N > 1 row bands and --band-of (band 0 of 8: cfg5 0.2140-0.2146 vs "
+                         "0.2244-0.2281 ms with 3, cfg2 within 1 %%; profiles/bands_inflight_r05.jsonl)")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the end-to-end host-buffer measurement (rank 0, N=1)")
     ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
@@ -452,7 +452,8 @@ def main():
     s0 = torch.from_numpy(L).to(dev)
     s1 = torch.from_numpy(R).to(dev)
     del L, R
-    F = max(1, args.inflight if args.inflight is not None else (2 if world == 1 else 3))
+    F = max(1, args.inflight if args.inflight is not None else
+            (2 if world == 1 and args.band_of == 1 else 6))
     # one engine (workspace) and one stream per frame in flight; slot 0 = torch's stream
     engines = [device.Engine(local_dev) for _ in range(F)]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(F - 1)]

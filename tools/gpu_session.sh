@@ -193,6 +193,16 @@ for step in "$@"; do
             run revprof_kept 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof_kept -o run --output-format csv -- python tools/random_search_bench.py --words 4 --inputs random_u128 --reps 5
             BICOS_REV_FULL=1 run revprof_full 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof_full -o run --output-format csv -- python tools/random_search_bench.py --words 4 --inputs random_u128 --reps 5 ;;
         hostdma) run hostdma 300 python tools/host_dma_probe.py ;;
+        bandfl)  # frames in flight for row bands: band 0 of BANDS-way splits of SCS configs, F = FLS, interleaved twice
+            for k in 1 2; do
+                for c in ${SCS:-cfg2 cfg5}; do
+                    for b in ${BANDS:-8 4}; do
+                        for f in ${FLS:-3 4 6}; do
+                            run bandfl_${c}_${b}_f${f}_$k 300 python bench.py --config $c --band-of $b --inflight $f --steps 100 --warmup 5 --no-cpu-baseline --no-host-path --kernel-reps 0
+                        done
+                    done
+                done
+            done ;;
         swband)  # search geometries for row bands (cfg2 N = 8 / 4 bands and the whole frame), back to back
             for r in ${ROWS:-192 384 1536}; do
                 run swband_$r 300 python tools/search_sweep.py --config ${SC:-cfg2} --rows $r --rounds 7 --reps 10 \
