@@ -1120,6 +1120,11 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
             "frac": main["frac"],
             "timing": "in frame: the average of %d searches timed with HIP events on their stream, "
                       "each after both transforms and before the agree, as in a match" % reps,
+            # the headline shape (engine.cpp fuse_agree, search_mx_agree_fusable) runs the agree
+            # inside this kernel's launch in the match itself; the search is timed alone here
+            "agree_fused_in_match": bool(mx and not pk and not cons and n == 33 and words == 4 and
+                                         C.get("dtype", "u8") == "u8" and not mc.get("precision")
+                                         and mc.get("subpixel_step") is None),
             "back_to_back": {"ms_per_launch": round(t_b2b * 1e3, 4),
                              "frac": round(main["frac"] * t_search / t_b2b, 4)},
             "reverse_col1_kept": kept,

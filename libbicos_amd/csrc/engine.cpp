@@ -109,6 +109,16 @@ bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, in
                                       e->tune_waves, e->tune_split, e->cus);
 }
 
+// The agree inside the search launch for the shape search_mx_agree_fusable accepts
+// (BICOS_FUSE_AGREE=0: the separate agree launch; read once)
+static bool fuse_agree() {
+    static const bool on = [] {
+        const char* v = std::getenv("BICOS_FUSE_AGREE");
+        return !(v && !std::strcmp(v, "0"));
+    }();
+    return on;
+}
+
 // Search implementation: the matrix-core search (search_mx.hip) unless the engine is tuned
 // to the VALU search (bicos_engine_tune variant 16) or BICOS_SEARCH=valu;
 // BICOS_SEARCH=mx forces it. Results are identical either way.
@@ -269,21 +279,6 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
         return check_hip(bicos_hip::launch_search(sa, geometry(e, rows, cols, words), words, nd, st),
                          what);
     };
-    if (!consistency) {
-        rc = search(d0, d1, raw, 0, true, "search launch");
-        if (rc) return rc;
-    } else {
-        rc = search(d0, d1, fwd, 1, nodupes, "search launch");
-        if (!rc)
-            rc = search(d1, d0, rev, 1, nodupes, "reverse search launch",
-                        reverse_compacted(mx) ? fwd : nullptr);
-        if (rc) return rc;
-        bicos_hip::ConsistencyArgs ca{fwd, rev, raw, rows, cols, (size_t)cols, cfg.max_lr_diff};
-        rc = check_hip(bicos_hip::launch_consistency(ca, st), "consistency launch");
-        if (rc) return rc;
-    }
-    if (!has_nxcorr) return BICOS_OK;
-
     // 3. agree / agree_subpixel (cpu.cpp:77-95)
     bicos_hip::AgreeArgs aa{};
     aa.raw = raw;
@@ -304,6 +299,35 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     aa.out_f32 = disp_i16 ? 0 : 1;
     aa.corrmap = corr;
     aa.stack_bytes = span;
+
+    // the headline shape runs the agree inside the search's workgroups (one launch,
+    // search_mx.hip fused_agree; BICOS_FUSE_AGREE=0 keeps the two launches)
+    const bool aligned4 = ((row_pitch | plane_pitch) & 3) == 0 &&
+                          (((uintptr_t)s0 | (uintptr_t)s1) & 3) == 0;
+    if (!consistency && has_nxcorr && !has_step && mx && aligned4 && fuse_agree()) {
+        const bicos_hip::MxGeometry g = mx_geometry(e, rows, cols, words, used_bits(n, mode));
+        if (bicos_hip::search_mx_agree_fusable(g, words, true, cols, n, depth, dbl)) {
+            bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0, 0};
+            sa.ag = aa;
+            return check_hip(bicos_hip::launch_search_mx_agree(sa, g, st), "search + agree launch");
+        }
+    }
+
+    if (!consistency) {
+        rc = search(d0, d1, raw, 0, true, "search launch");
+        if (rc) return rc;
+    } else {
+        rc = search(d0, d1, fwd, 1, nodupes, "search launch");
+        if (!rc)
+            rc = search(d1, d0, rev, 1, nodupes, "reverse search launch",
+                        reverse_compacted(mx) ? fwd : nullptr);
+        if (rc) return rc;
+        bicos_hip::ConsistencyArgs ca{fwd, rev, raw, rows, cols, (size_t)cols, cfg.max_lr_diff};
+        rc = check_hip(bicos_hip::launch_consistency(ca, st), "consistency launch");
+        if (rc) return rc;
+    }
+    if (!has_nxcorr) return BICOS_OK;
+
     if (has_step)
         rc = check_hip(bicos_hip::launch_subpixel(aa, depth, dbl, st), "subpixel launch");
     else

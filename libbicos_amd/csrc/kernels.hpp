@@ -21,6 +21,24 @@ struct TransformArgs {
     uint32_t stack_bytes;   // bytes addressable from each stack base (< 4 GiB)
 };
 
+struct AgreeArgs {
+    const int16_t* raw;     // integer disparity from the search
+    size_t raw_pitch;
+    const void* stack0;
+    const void* stack1;
+    int n, rows, cols;
+    size_t row_pitch, plane_pitch;
+    float threshold;
+    float step;             // subpixel only
+    int nsteps;             // subpixel only: x = -1, -1+step, ... <= 1 (subpixel_steps)
+    int has_minvar;
+    float minvar;           // already scaled by n (reference cpu.cpp:127)
+    void* out;              // dense [rows][cols]
+    int out_f32;            // agree: 1 -> float32 output, 0 -> int16 in place semantics
+    void* corrmap;          // dense [rows][cols] float (double for DOUBLE) or nullptr
+    uint32_t stack_bytes;   // bytes addressable from each stack base (< 4 GiB)
+};
+
 struct SearchArgs {
     const uint32_t* desc0;  // the side whose pixels are matched (col0)
     const uint32_t* desc1;  // the side that is searched (col1)
@@ -40,6 +58,9 @@ struct SearchArgs {
     // (keep = the forward result, best col1 or -1; reference bicos.hpp:94-101)
     const int16_t* keep;
     size_t keep_pitch;      // int16 elements
+    // launch_search_mx_agree only: the agree stage (ag.raw unused) run by each workgroup over
+    // its own col0 once their search is done
+    AgreeArgs ag;
 };
 
 struct SearchGeometry {
@@ -60,23 +81,6 @@ struct ConsistencyArgs {
     int max_lr_diff;
 };
 
-struct AgreeArgs {
-    const int16_t* raw;     // integer disparity from the search
-    size_t raw_pitch;
-    const void* stack0;
-    const void* stack1;
-    int n, rows, cols;
-    size_t row_pitch, plane_pitch;
-    float threshold;
-    float step;             // subpixel only
-    int nsteps;             // subpixel only: x = -1, -1+step, ... <= 1 (subpixel_steps)
-    int has_minvar;
-    float minvar;           // already scaled by n (reference cpu.cpp:127)
-    void* out;              // dense [rows][cols]
-    int out_f32;            // agree: 1 -> float32 output, 0 -> int16 in place semantics
-    void* corrmap;          // dense [rows][cols] float (double for DOUBLE) or nullptr
-    uint32_t stack_bytes;   // bytes addressable from each stack base (< 4 GiB)
-};
 
 hipError_t launch_transform(TransformArgs a, int depth, int mode, int words, hipStream_t st);
 SearchGeometry search_geometry(int rows, int cols, int words, int max_lds_bytes, int variant = 16,
@@ -87,7 +91,7 @@ hipError_t launch_search(SearchArgs a, const SearchGeometry& g, int words, bool 
 hipError_t launch_consistency(const ConsistencyArgs& a, hipStream_t st);
 
 // Matrix-core search (search_mx.hip): FP4 MFMA Hamming products, argmin keys in the
-// accumulator. Same outputs as launch_search (a.out, a.out_mode); no fused agree.
+// accumulator. Same outputs as launch_search (a.out, a.out_mode).
 struct MxGeometry {
     int chunk;              // col1 per LDS fill (multiple of 32)
     int waves;              // waves per workgroup
@@ -118,6 +122,14 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
                               int waves = 0, int cus = 256, int keys = 0, int bits = 0);
 hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool nodupes,
                             hipStream_t st);
+// The agree stage fused into the search (one launch): each workgroup, once its waves have
+// their col0's results, runs launch_agree's arithmetic over those col0 (a.ag; outputs as
+// launch_agree's, a.out still gets the integer map). Only the shape it is built for: 128-bit
+// NoDuplicates search, 4 tiles per wave, no tail launch, u8 stacks of n = 33, float, no
+// subpixel step; search_mx_agree_fusable says whether g / the match are that shape.
+bool search_mx_agree_fusable(const MxGeometry& g, int words, bool nodupes, int cols, int n,
+                             int depth, bool dbl);
+hipError_t launch_search_mx_agree(SearchArgs a, const MxGeometry& g, hipStream_t st);
 hipError_t launch_agree(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
 hipError_t launch_subpixel(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
 // n > 40 (subpixel_wide.hip); launch_subpixel dispatches to it

@@ -30,6 +30,8 @@
 // ds_read_b128 per lane. Accumulator map (32x32 shapes): lane l, register r holds row
 // (r & 3) + 8 (r >> 2) + 4 (l >> 5) (= col1 in the block) and column l & 31 (= col0).
 #include "kernels.hpp"
+#include "nxc.hpp"
+#include "stack.hpp"
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -367,8 +369,71 @@ inline int list_grid(int rows, int tiles_per_row) {
 #define BICOS_REV_AHEAD_CHUNK 0
 #endif
 constexpr int REV_AHEAD = BICOS_REV_AHEAD;
+
+// The agree stage (kernels.hip agree_reg_kernel, reference agree.hpp:53-93: NXC of the n left
+// samples at col and the n right ones at col - d, invalid below the threshold) for the cnt
+// col0 from c0 of one row whose integer disparities the workgroup holds in LDS, u8 stacks,
+// float, n = N exactly: the search_mx_kernel AG epilogue. Same arithmetic, order and outputs
+// as agree_reg_kernel<uint8_t, float, N, true>, so the two are interchangeable bit for bit.
+// (Staging the left samples in LDS with dword loads and gathering two pixels' right samples
+// per thread before either's arithmetic, as agree_lds_kernel does, measured slower here:
+// the fused launch 351 vs 345 us at cfg2, profiles/fused_agree_r05.jsonl.)
+template <int N>
+__device__ __forceinline__ void fused_agree(const AgreeArgs& g, int row, int c0, int cnt,
+                                            const int16_t* raw) {
+    const StackReader<uint8_t> rd0(g.stack0, g.stack_bytes), rd1(g.stack1, g.stack_bytes);
+    const uint32_t rowoff = (uint32_t)row * (uint32_t)g.row_pitch;
+    const uint32_t pp = (uint32_t)g.plane_pitch;
+    const int cols = g.cols;
+    for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+        const int col = c0 + i;
+        int d = raw[i];
+        const int idx1 = col - d;
+        const bool inb = d != INVALID_I16 && idx1 >= 0 && idx1 < cols;
+        uint32_t l[N], r[N];
+        uint32_t sl = 0, sr = 0;
+#pragma unroll
+        for (int t = 0; t < N; ++t) l[t] = rd0((uint32_t)col, rowoff + (uint32_t)t * pp);
+        const uint32_t c1 = inb ? (uint32_t)idx1 : (uint32_t)col;
+#pragma unroll
+        for (int t = 0; t < N; ++t) r[t] = rd1(c1, rowoff + (uint32_t)t * pp);
+#pragma unroll
+        for (int t = 0; t < N; ++t) {
+            sl += l[t];
+            sr += r[t];
+        }
+        float corr = __builtin_nanf("");
+        if (inb) {
+            const float m0 = nxc::div_p((float)sl, (float)N);
+            const float m1 = nxc::div_p((float)sr, (float)N);
+            float cov = 0.f, v0 = 0.f, v1 = 0.f;
+#pragma unroll
+            for (int t = 0; t < N; ++t) {
+                const float x0 = (float)l[t] - m0;
+                const float x1 = (float)r[t] - m1;
+                cov = nxc::fma_p(x0, x1, cov);
+                v0 = nxc::fma_p(x0, x0, v0);
+                v1 = nxc::fma_p(x1, x1, v1);
+            }
+            if (g.has_minvar && (v0 < g.minvar || v1 < g.minvar))
+                corr = -1.f;
+            else
+                corr = nxc::div_p(cov, nxc::sqrt_p(v0 * v1));
+            if (corr < g.threshold) d = INVALID_I16;  // NaN passes, as in the reference
+        } else {
+            d = INVALID_I16;
+        }
+        const size_t o = (size_t)row * cols + col;
+        if (g.out_f32)
+            ((float*)g.out)[o] = (float)d;
+        else
+            ((int16_t*)g.out)[o] = (int16_t)d;
+        if (g.corrmap) ((float*)g.corrmap)[o] = corr;
+    }
+}
+constexpr int FUSED_AGREE_N = 33;
 constexpr int REV_AHEAD_CHUNK = BICOS_REV_AHEAD_CHUNK;
-template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIST>
+template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIST, bool AG = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KSU >= 4 ? 3 : 4)))
 void search_mx_kernel(SearchArgs a) {
     constexpr bool FK = KEYS == 3;
@@ -784,7 +849,12 @@ void search_mx_kernel(SearchArgs a) {
             }
         }
     }
-    if (idle) return;
+    if (!AG && idle) return;
+    // AG: the workgroup's integer results go through LDS to the fused agree below; the chunk
+    // region is reused once every wave is done with its blocks
+    int16_t* raw_lds = reinterpret_cast<int16_t*>(lds_mx);
+    const int wg_c0 = c0_base + tile * waves * T * 32;
+    if constexpr (AG) __syncthreads();
 
     // the two lane halves hold the even / odd 4-row groups of every block
 #pragma unroll
@@ -824,7 +894,7 @@ void search_mx_kernel(SearchArgs a) {
     for (int t = 0; t < T; ++t) {
         if ((t & 1) != h) continue;  // half 0 writes even tiles, half 1 odd tiles
         const int c0i = c0_wave + 32 * t + jo;
-        if (c0i >= lcols) continue;
+        if (idle || c0i >= lcols) continue;
         const int c0 = lcol(c0i);
         const int best = best_of(t);
         const bool ok = unique_of(t, best);
@@ -834,6 +904,11 @@ void search_mx_kernel(SearchArgs a) {
         else
             v = ok ? (int16_t)best : (int16_t)-1;
         out[c0] = v;
+        if constexpr (AG) raw_lds[c0 - wg_c0] = v;
+    }
+    if constexpr (AG) {
+        __syncthreads();
+        fused_agree<FUSED_AGREE_N>(a.ag, row, wg_c0, min(waves * T * 32, cols - wg_c0), raw_lds);
     }
 }
 
@@ -1218,12 +1293,12 @@ hipError_t launch_pk_w(const SearchArgs& a, const MxGeometry& g, hipStream_t st)
     return hipErrorInvalidValue;
 }
 
-template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIST = false>
+template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIST = false, bool AG = false>
 hipError_t launch_mx_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st) {
     constexpr int WL = 2 * KSU;
     size_t lds = (size_t)WL * a.chunk * 16;
     if (LIST) lds = list_ent_offset((int)lds) + (size_t)waves * T * 32 * 2;
-    const auto kern = search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, TAIL, LIST>;
+    const auto kern = search_mx_kernel<WORDS, KSU, NODUPES, T, KEYS, TAIL, LIST, AG>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1410,6 +1485,27 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
         g.pk_tail_col0 = (int)(cols - pk_rem);
     }
     return g;
+}
+
+bool search_mx_agree_fusable(const MxGeometry& g, int words, bool nodupes, int cols, int n,
+                             int depth, bool dbl) {
+    // launch_mx_t's key choice for this shape is KEYS 2 (NoDuplicates, cols <= XKF_MAX_COLS)
+    return !g.pk && words == 4 && g.ksteps == 2 && nodupes && g.keys == 1 &&
+           cols <= XKF_MAX_COLS && g.T == 4 && g.tail_T == 0 && n == FUSED_AGREE_N &&
+           depth == 1 && !dbl && g.chunk * 4 * 16 >= 2 * 32 * 4 * g.waves;  // raw in LDS
+}
+
+hipError_t launch_search_mx_agree(SearchArgs a, const MxGeometry& g, hipStream_t st) {
+    if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
+    if (a.keep || a.out_mode != 0 || a.cols > 32767 || g.chunk < 32 || (g.chunk & 31) ||
+        g.waves < 1 || g.waves > 8 || g.T != 4 || g.tail_T != 0)
+        return hipErrorInvalidValue;
+    a.chunk = g.chunk;
+    const long per_wg = 32L * g.waves * 4;
+    a.tiles_per_row = (int)((a.cols + per_wg - 1) / per_wg);
+    a.tail_T = 0;
+    a.tail_col0 = a.cols;
+    return launch_mx_grid<4, 2, true, 4, 2, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st);
 }
 
 hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool nodupes,

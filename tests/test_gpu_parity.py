@@ -1201,3 +1201,34 @@ def test_int16_disparity_rejects_subpixel(gpu):
     with pytest.raises(ValueError):
         gpu.match(dev(L), dev(R), MatchConfig(subpixel_step=0.1),
                   out=torch.empty((16, 64), dtype=torch.int16, device="cuda"))
+
+
+# ------------------- agree fused into the search launch (search_mx.hip fused_agree, round 5)
+# The headline shape (128-bit NoDuplicates search with 4 tiles per wave and no tail launch,
+# u8 stacks of n = 33, float, no subpixel) runs the agree inside the search's workgroups.
+# Frames tall enough for that geometry (300 rows x 1800 / 2048 columns: >= 2 workgroups per
+# CU, no tail; the last workgroup of an 1800-column row holds 776 col0) against the separate
+# search + agree stages (the stage API launches them apart), with and without min-variance,
+# float32 and int16 disparity maps; the whole-frame cfg2 / cfg5 tests pin it to the oracle.
+@pytest.mark.parametrize("W", [1800, 2048])
+@pytest.mark.parametrize("kw", [dict(nxcorr_threshold=0.96),
+                                dict(nxcorr_threshold=0.5, min_variance=2.0)])
+def test_fused_search_agree_equals_stages(gpu, W, kw):
+    import torch
+    from libbicos_amd.device import MatchConfig, descriptor_words
+    n, H = 33, 300
+    L, R = stereo_stack(n, H, W, np.uint8, dmin=3, drange=40, seed=W + len(kw))
+    L[:, 5, 200:260] = 9  # flat patch: NaN / low-variance correlations
+    s0, s1 = dev(L), dev(R)
+    cfg = MatchConfig(**kw)
+    md, mc = gpu.match(s0, s1, cfg)
+    words = descriptor_words(n, 0)
+    raw = gpu.search(gpu.transform(s0, 0, words), gpu.transform(s1, 0, words), W, words, 1)
+    mv = float(np.float32(kw["min_variance"]) * np.float32(n)) if "min_variance" in kw else None
+    ad, ac = gpu.agree(raw, s0, s1, kw["nxcorr_threshold"], mv)
+    same(host(md), host(ad))
+    same(host(mc), host(ac))
+    io = torch.empty((H, W), dtype=torch.int16, device="cuda")
+    io, ic = gpu.match(s0, s1, cfg, out=io)
+    same(host(io).astype(np.float32), host(md))
+    same(host(ic), host(mc))

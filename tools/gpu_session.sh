@@ -193,6 +193,14 @@ for step in "$@"; do
             run revprof_kept 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof_kept -o run --output-format csv -- python tools/random_search_bench.py --words 4 --inputs random_u128 --reps 5
             BICOS_REV_FULL=1 run revprof_full 300 rocprofv3 --kernel-trace --stats -d gpurun_out/revprof_full -o run --output-format csv -- python tools/random_search_bench.py --words 4 --inputs random_u128 --reps 5 ;;
         hostdma) run hostdma 300 python tools/host_dma_probe.py ;;
+        fuseab)  # agree fused into the search launch vs separate (BICOS_FUSE_AGREE=0), SCS configs, interleaved REPS times
+            for k in $(seq ${REPS:-2}); do
+                for c in ${SCS:-cfg2}; do
+                    run fuse_${c}_on$k 300 python bench.py --config $c --steps 40 --warmup 3 --no-cpu-baseline --no-host-path ${BARGS:-}
+                    BICOS_FUSE_AGREE=0 run fuse_${c}_off$k 300 python bench.py --config $c --steps 40 --warmup 3 --no-cpu-baseline --no-host-path ${BARGS:-}
+                done
+            done
+            run fuseprof 300 rocprofv3 --kernel-trace --stats -d gpurun_out/fuseprof -o run --output-format csv -- python bench.py --config ${SC:-cfg2} --steps 10 --warmup 2 --inflight 1 --no-cpu-baseline --no-host-path --kernel-reps 0 ;;
         bandfl)  # frames in flight for row bands: band 0 of BANDS-way splits of SCS configs, F = FLS, interleaved twice
             for k in 1 2; do
                 for c in ${SCS:-cfg2 cfg5}; do
