@@ -1088,6 +1088,9 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
         mark = torch.zeros((rows, W + 1), dtype=torch.bool, device=dev)
         mark.scatter_(1, torch.where(ok, c0 - fwd.long(), torch.full_like(c0, W)), True)
         kept = float(mark[:, :W].sum().item())
+    fused = bool(mx and not pk and not cons and n == 33 and words == 4 and
+                 C.get("dtype", "u8") == "u8" and not mc.get("precision") and
+                 mc.get("subpixel_step") is None)
     if mx:
         alg_flops, used_flops = mx_flops(rows, W, words, mc, ubits, sbits, reverse_col1=kept)
         achieved_tf = alg_flops / t_search / 1e12
@@ -1122,14 +1125,16 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
                       "each after both transforms and before the agree, as in a match" % reps,
             # the headline shape (engine.cpp fuse_agree, search_mx_agree_fusable) runs the agree
             # inside this kernel's launch in the match itself; the search is timed alone here
-            "agree_fused_in_match": bool(mx and not pk and not cons and n == 33 and words == 4 and
-                                         C.get("dtype", "u8") == "u8" and not mc.get("precision")
-                                         and mc.get("subpixel_step") is None),
+            "agree_fused_in_match": fused,
             "back_to_back": {"ms_per_launch": round(t_b2b * 1e3, 4),
                              "frac": round(main["frac"] * t_search / t_b2b, 4)},
             "reverse_col1_kept": kept,
             "traffic": traffic["bytes"],
             "traffic_source": traffic.get("source") or traffic.get("why"),
+            # fused: the PMC bytes are the one launch's, search + agree, against both stages'
+            # algorithmic bytes
+            "traffic_covers": "search + agree (one fused launch)" if fused else "search",
+            "algorithmic_bytes_traffic_covers": search_bytes + ag_bytes if fused else search_bytes,
             "algorithmic_bytes": search_bytes,
             "algorithmic_flops": alg_flops,
             "k_bits_per_pair": k_exec,

@@ -43,10 +43,11 @@ def bench_table():
         d = L[c]
         r = d["roofline"]
         h = r["hbm"]
-        search = "%.4f ms in frame (%.4f back to back), %s; PMC %s MB (algorithmic %.1f)" % (
+        search = "%.4f ms in frame (%.4f back to back), %s; PMC %s%s MB (algorithmic %.1f)" % (
             r["ms_per_launch"], r["back_to_back"]["ms_per_launch"], bound_text(r),
+            "search + agree, one launch: " if r.get("agree_fused_in_match") else "",
             "%.1f" % (r["traffic"] / 1e6) if r.get("traffic") else "n/a",
-            r["algorithmic_bytes"] / 1e6)
+            r.get("algorithmic_bytes_traffic_covers", r["algorithmic_bytes"]) / 1e6)
         if c == "cfg4":
             search += "; %.3f on used bits" % r["used_bits_view"]["frac"]
         if "subpixel" in r:
