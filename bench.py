@@ -1088,9 +1088,10 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
         mark = torch.zeros((rows, W + 1), dtype=torch.bool, device=dev)
         mark.scatter_(1, torch.where(ok, c0 - fwd.long(), torch.full_like(c0, W)), True)
         kept = float(mark[:, :W].sum().item())
-    fused = bool(mx and not pk and not cons and n == 33 and words == 4 and
-                 C.get("dtype", "u8") == "u8" and not mc.get("precision") and
-                 mc.get("subpixel_step") is None)
+    # (search_mx_agree_fusable: the 128-bit shape of cfg2 / cfg5, the packed-key one of cfg1)
+    fused = bool(mx and not cons and C.get("dtype", "u8") == "u8" and not mc.get("precision")
+                 and mc.get("subpixel_step") is None and
+                 ((not pk and n == 33 and words == 4) or (pk and n == 8 and words == 1)))
     if mx:
         alg_flops, used_flops = mx_flops(rows, W, words, mc, ubits, sbits, reverse_col1=kept)
         achieved_tf = alg_flops / t_search / 1e12

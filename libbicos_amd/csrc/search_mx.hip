@@ -431,7 +431,8 @@ __device__ __forceinline__ void fused_agree(const AgreeArgs& g, int row, int c0,
         if (g.corrmap) ((float*)g.corrmap)[o] = corr;
     }
 }
-constexpr int FUSED_AGREE_N = 33;
+constexpr int FUSED_AGREE_N = 33;    // search_mx_kernel AG: 128-bit descriptors (cfg2, cfg5)
+constexpr int FUSED_AGREE_N_PK = 8;  // search_pk_kernel AG: 32-bit descriptors (cfg1)
 constexpr int REV_AHEAD_CHUNK = BICOS_REV_AHEAD_CHUNK;
 template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIST, bool AG = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KSU >= 4 ? 3 : 4)))
@@ -1014,10 +1015,11 @@ __device__ __forceinline__ v16f mfma_pk(v4i a, v4i b, v16f c, int sb) {
 // T wide tiles (64 col0 each) per wave; T = 1 or an even count (tiles reduced in pairs);
 // TAIL: the col0 range starts at a.tail_col0 (the tail launch, as search_mx_kernel's);
 // LIST: compacted col0 entries (as search_mx_kernel's)
-template <int WORDS, int T, bool TAIL, bool LIST>
+template <int WORDS, int T, bool TAIL, bool LIST, bool AG = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void search_pk_kernel(SearchArgs a) {
     static_assert(T == 1 || T % 2 == 0, "wide tiles: 1 or pairs");
+    static_assert(!AG || (!TAIL && !LIST), "the fused agree: main launch, every col0");
     constexpr int NP = T == 1 ? 1 : T / 2;
     extern __shared__ __attribute__((aligned(16))) v4i lds_mx[];  // [WORDS][chunk]
 
@@ -1203,7 +1205,12 @@ void search_pk_kernel(SearchArgs a) {
             block(b, false);
         }
     }
-    if (idle) return;
+    if (!AG && idle) return;
+    // AG: the workgroup's integer results go through LDS to the fused agree (as in
+    // search_mx_kernel); the chunk region is reused once every wave is done with its blocks
+    int16_t* raw_lds = reinterpret_cast<int16_t*>(lds_mx);
+    const int wg_c0 = c0_base + tile * waves * T * 64;
+    if constexpr (AG) __syncthreads();
 
     int16_t* out = a.out + (size_t)row * a.out_pitch;
     int jo = j;
@@ -1215,7 +1222,7 @@ void search_pk_kernel(SearchArgs a) {
 #pragma unroll
         for (int f = 0; f < 2; ++f) {  // f = 0: high field (col0 P), 1: low field (Q = P + 32)
             const int c0i = c0_wave + 64 * t + 32 * f + jo;
-            if (c0i >= lcols) continue;
+            if (idle || c0i >= lcols) continue;
             const int c0 = lcol(c0i);
             const int sh = f ? 0 : 16;
             const int best = (int)((C[p] >> sh) & 0xFFFFu);
@@ -1226,15 +1233,20 @@ void search_pk_kernel(SearchArgs a) {
             else
                 v = ok ? (int16_t)best : (int16_t)-1;
             out[c0] = v;
+            if constexpr (AG) raw_lds[c0 - wg_c0] = v;
         }
+    }
+    if constexpr (AG) {
+        __syncthreads();
+        fused_agree<FUSED_AGREE_N_PK>(a.ag, row, wg_c0, min(waves * T * 64, cols - wg_c0), raw_lds);
     }
 }
 
-template <int WORDS, int T, bool TAIL, bool LIST = false>
+template <int WORDS, int T, bool TAIL, bool LIST = false, bool AG = false>
 hipError_t launch_pk_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st) {
     size_t lds = (size_t)WORDS * a.chunk * 16;
     if (LIST) lds = list_ent_offset((int)lds) + (size_t)waves * T * 64 * 2;
-    const auto kern = search_pk_kernel<WORDS, T, TAIL, LIST>;
+    const auto kern = search_pk_kernel<WORDS, T, TAIL, LIST, AG>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1489,14 +1501,30 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
 
 bool search_mx_agree_fusable(const MxGeometry& g, int words, bool nodupes, int cols, int n,
                              int depth, bool dbl) {
+    if (!nodupes || depth != 1 || dbl) return false;
+    // packed keys, 32-bit words, one wide tile per wave, no tail; the raw results (64 int16
+    // per wave) in the LDS stage (16 B per col1)
+    if (g.pk)
+        return words == 1 && g.pk_T == 1 && g.pk_tail_col0 == cols && n == FUSED_AGREE_N_PK &&
+               cols <= PK_MAX_COLS && g.pk_chunk * 16 >= 128 * g.waves;
     // launch_mx_t's key choice for this shape is KEYS 2 (NoDuplicates, cols <= XKF_MAX_COLS)
-    return !g.pk && words == 4 && g.ksteps == 2 && nodupes && g.keys == 1 &&
-           cols <= XKF_MAX_COLS && g.T == 4 && g.tail_T == 0 && n == FUSED_AGREE_N &&
-           depth == 1 && !dbl && g.chunk * 4 * 16 >= 2 * 32 * 4 * g.waves;  // raw in LDS
+    return words == 4 && g.ksteps == 2 && g.keys == 1 && cols <= XKF_MAX_COLS && g.T == 4 &&
+           g.tail_T == 0 && n == FUSED_AGREE_N &&
+           g.chunk * 4 * 16 >= 2 * 32 * 4 * g.waves;  // raw in LDS
 }
 
 hipError_t launch_search_mx_agree(SearchArgs a, const MxGeometry& g, hipStream_t st) {
     if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
+    if (g.pk) {
+        if (a.keep || a.out_mode != 0 || a.cols > PK_MAX_COLS || g.pk_chunk < 32 ||
+            (g.pk_chunk & 31) || g.waves < 1 || g.waves > 8 || g.pk_T != 1 || g.pk_tail_col0 != a.cols)
+            return hipErrorInvalidValue;
+        a.chunk = g.pk_chunk;
+        a.tiles_per_row = g.pk_tiles_per_row;
+        a.tail_T = 0;
+        a.tail_col0 = a.cols;
+        return launch_pk_grid<1, 1, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st);
+    }
     if (a.keep || a.out_mode != 0 || a.cols > 32767 || g.chunk < 32 || (g.chunk & 31) ||
         g.waves < 1 || g.waves > 8 || g.T != 4 || g.tail_T != 0)
         return hipErrorInvalidValue;

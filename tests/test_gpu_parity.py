@@ -1232,3 +1232,28 @@ def test_fused_search_agree_equals_stages(gpu, W, kw):
     io, ic = gpu.match(s0, s1, cfg, out=io)
     same(host(io).astype(np.float32), host(md))
     same(host(ic), host(mc))
+
+
+# The packed-key search's fused agree (search_pk_kernel AG: 32-bit words, one wide tile per
+# wave, no tail, u8 n = 8 -- cfg1's shape), against the separate stages as above; 700 columns
+# leave the row's second workgroup 188 col0.
+@pytest.mark.parametrize("H,W", [(480, 640), (100, 700)])
+def test_fused_pk_search_agree_equals_stages(gpu, H, W):
+    import torch
+    from libbicos_amd.device import MatchConfig, descriptor_words
+    n = 8
+    L, R = stereo_stack(n, H, W, np.uint8, dmin=3, drange=40, seed=H + W)
+    L[:, 3, 100:150] = 11  # flat patch
+    s0, s1 = dev(L), dev(R)
+    cfg = MatchConfig(nxcorr_threshold=0.9)
+    md, mc = gpu.match(s0, s1, cfg)
+    words = descriptor_words(n, 0)
+    d0, d1 = gpu.transform(s0, 0, words), gpu.transform(s1, 0, words)
+    raw = gpu.search(d0, d1, W, words, 1, bits=4 * n - 5)
+    ad, ac = gpu.agree(raw, s0, s1, 0.9)
+    same(host(md), host(ad))
+    same(host(mc), host(ac))
+    io = torch.empty((H, W), dtype=torch.int16, device="cuda")
+    io, ic = gpu.match(s0, s1, cfg, out=io)
+    same(host(io).astype(np.float32), host(md))
+    same(host(ic), host(mc))
