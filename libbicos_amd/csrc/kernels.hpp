@@ -125,7 +125,7 @@ hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool n
 // The agree stage fused into the search (one launch): each workgroup, once its waves have
 // their col0's results, runs launch_agree's arithmetic over those col0 (a.ag; outputs as
 // launch_agree's, a.out still gets the integer map). Only the shapes it is built for: the
-// 128-bit NoDuplicates search with 4 tiles per wave and no tail launch over u8 stacks of n =
+// 128-bit NoDuplicates search with 4 or 2 tiles per wave and no tail launch over u8 stacks of n =
 // 33, and the packed-key 32-bit search with one wide tile per wave and no tail over u8 stacks
 // of n = 8; float, no subpixel step. search_mx_agree_fusable says whether g / the match are one.
 bool search_mx_agree_fusable(const MxGeometry& g, int words, bool nodupes, int cols, int n,

@@ -1508,9 +1508,9 @@ bool search_mx_agree_fusable(const MxGeometry& g, int words, bool nodupes, int c
         return words == 1 && g.pk_T == 1 && g.pk_tail_col0 == cols && n == FUSED_AGREE_N_PK &&
                cols <= PK_MAX_COLS && g.pk_chunk * 16 >= 128 * g.waves;
     // launch_mx_t's key choice for this shape is KEYS 2 (NoDuplicates, cols <= XKF_MAX_COLS)
-    return words == 4 && g.ksteps == 2 && g.keys == 1 && cols <= XKF_MAX_COLS && g.T == 4 &&
-           g.tail_T == 0 && n == FUSED_AGREE_N &&
-           g.chunk * 4 * 16 >= 2 * 32 * 4 * g.waves;  // raw in LDS
+    return words == 4 && g.ksteps == 2 && g.keys == 1 && cols <= XKF_MAX_COLS &&
+           (g.T == 4 || g.T == 2) && g.tail_T == 0 && n == FUSED_AGREE_N &&
+           g.chunk * 4 * 16 >= 2 * 32 * g.T * g.waves;  // raw in LDS
 }
 
 hipError_t launch_search_mx_agree(SearchArgs a, const MxGeometry& g, hipStream_t st) {
@@ -1526,13 +1526,16 @@ hipError_t launch_search_mx_agree(SearchArgs a, const MxGeometry& g, hipStream_t
         return launch_pk_grid<1, 1, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st);
     }
     if (a.keep || a.out_mode != 0 || a.cols > 32767 || g.chunk < 32 || (g.chunk & 31) ||
-        g.waves < 1 || g.waves > 8 || g.T != 4 || g.tail_T != 0)
+        g.waves < 1 || g.waves > 8 || (g.T != 4 && g.T != 2) || g.tail_T != 0)
         return hipErrorInvalidValue;
     a.chunk = g.chunk;
-    const long per_wg = 32L * g.waves * 4;
+    const long per_wg = 32L * g.waves * g.T;
     a.tiles_per_row = (int)((a.cols + per_wg - 1) / per_wg);
     a.tail_T = 0;
     a.tail_col0 = a.cols;
+    // 2 tiles per wave: narrow row bands (N = 8 bands of cfg2, 192 rows)
+    if (g.T == 2)
+        return launch_mx_grid<4, 2, true, 2, 2, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st);
     return launch_mx_grid<4, 2, true, 4, 2, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st);
 }
 

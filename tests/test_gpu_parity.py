@@ -1210,14 +1210,15 @@ def test_int16_disparity_rejects_subpixel(gpu):
 # CU, no tail; the last workgroup of an 1800-column row holds 776 col0) against the separate
 # search + agree stages (the stage API launches them apart), with and without min-variance,
 # float32 and int16 disparity maps; the whole-frame cfg2 / cfg5 tests pin it to the oracle.
-@pytest.mark.parametrize("W", [1800, 2048])
+# 60 / 40 rows: small grids take 2 tiles per wave (the N = 8 band shape), also fused.
+@pytest.mark.parametrize("H,W", [(300, 1800), (300, 2048), (60, 2048), (40, 1800)])
 @pytest.mark.parametrize("kw", [dict(nxcorr_threshold=0.96),
                                 dict(nxcorr_threshold=0.5, min_variance=2.0)])
-def test_fused_search_agree_equals_stages(gpu, W, kw):
+def test_fused_search_agree_equals_stages(gpu, H, W, kw):
     import torch
     from libbicos_amd.device import MatchConfig, descriptor_words
-    n, H = 33, 300
-    L, R = stereo_stack(n, H, W, np.uint8, dmin=3, drange=40, seed=W + len(kw))
+    n = 33
+    L, R = stereo_stack(n, H, W, np.uint8, dmin=3, drange=40, seed=W + H + len(kw))
     L[:, 5, 200:260] = 9  # flat patch: NaN / low-variance correlations
     s0, s1 = dev(L), dev(R)
     cfg = MatchConfig(**kw)
