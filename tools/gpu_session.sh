@@ -186,7 +186,7 @@ for step in "$@"; do
                         proxy*) extra="--root-load proxy --root-load-wgs ${m#proxy}" ;;
                         *) extra="--root-load $m" ;;
                     esac
-                    run rl_${c}_${m}$k 300 python bench.py --config $c --band-of ${RLN:-8} --inflight 3 --steps 400 --warmup 10 --no-cpu-baseline --no-host-path --kernel-reps 0 $extra
+                    run rl_${c}_${RLN:-8}_${m}$k 300 python bench.py --config $c --band-of ${RLN:-8} --inflight ${INFL:-3} --steps 400 --warmup 10 --no-cpu-baseline --no-host-path --kernel-reps 0 $extra
                 done
             done; done ;;
         revprof)  # kernel trace of the random-descriptor searches: kept col1 / full reverse
