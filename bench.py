@@ -11,8 +11,8 @@ to rank 0 with ONE RCCL gather per step, inside the timed region; the gather of
 step k overlaps the kernels of step k+1 (double-buffered), and every gather has
 completed before the closing barrier.
 
-Frames in flight (--inflight F; default 2 for one GPU, 6 for row bands on N > 1): step k
-runs on stream k % F with its own
+Frames in flight (--inflight F; on one GPU per config -- 1 for cfg2 / cfg4 / cfg5, 2 for
+cfg1 / cfg3 -- and 6 for row bands on N > 1): step k runs on stream k % F with its own
 engine and output buffers, so consecutive frames overlap the way a camera stream is
 processed -- the HBM-bound transform / agree of one frame fill the compute-unit slots the
 previous frame's search leaves idle in its last round of workgroups (narrow row bands:
@@ -117,6 +117,19 @@ for (_n, _s), _ms in INTEG_RTX4090_MS.items():
 del _n, _s, _ms, _cfg
 
 
+# Frames in flight at N = 1, per config: F = 1 / 2 / 3 interleaved twice in
+# one session at the driver's 20 steps and at 200 (profiles/inflight_r06.jsonl). A config
+# keeps 2 only where 2 won by more than the run-to-run spread (~1.3 %): cfg1 (launch-bound:
+# 13030 vs 9729 Mpix/s at F = 1), cfg3 (the subpixel refine overlaps the next frame's search:
+# +2.6 %). cfg2 / cfg4 / cfg5: F = 1 (cfg2 7740 vs 7668 at 20 steps, 7751 vs 7824 at 200;
+# cfg5 4741 vs 4693). Other configs: 1, unless listed.
+INFLIGHT_DEFAULT = {"cfg1": 2, "cfg3": 2}
+
+
+def inflight_default(config: str) -> int:
+    return INFLIGHT_DEFAULT.get(config, 1)
+
+
 def search_pairs(rows: int, W: int, cfg: dict) -> float:
     """Hamming pairs of one pass over the cost matrix: every (col0, col1) of every row.
     Consistency searches it twice (forward, then the full reverse; callers double it)."""
@@ -208,15 +221,41 @@ def pk_key_pair_peak() -> float:
     return 1.0 / (full / (VALU_FULL_TOPS * 1e12) + half / (VALU_HALF_TOPS * 1e12))
 
 
-def mx_key_pair_peak(words: int, cfg: dict) -> float:
-    """Issue bound in pairs/s of the matrix-core search's VALU key reduction at the
-    measured rates: per pair 1/2 v_min3 (half rate) for the first minimum and, with
-    NoDuplicates, one v_xor (full) + 1/2 v_min3 for the last minimum; per 32-pair tile
-    column 1-2 integer adds (full; negligible)."""
+# Fraction of (tile, block) units of the NoDuplicates search that take the last-minimum
+# branch on the planted-disparity frames: ~5.6 reaching blocks per tile and row scan whatever
+# the width (tools/reach_sim.py: 2048 columns 0.068 / 0.094 / 0.103 at rows 0 / 767 / 1535,
+# 3840 columns 0.047), i.e. ~180 / cols; random descriptors reach on ~0.73.
+def mx_reach_planted(cols: int) -> float:
+    return min(1.0, 180.0 / max(cols, 1))
+
+
+MX_REACH_PLANTED = mx_reach_planted(2048)
+
+
+def mx_key_pair_peak(words: int, cfg: dict, reach: float = MX_REACH_PLANTED) -> float:
+    """Issue bound in pairs/s of the matrix-core search's VALU key reduction AS EXECUTED, at
+    the measured rates: the instructions per (wave, 32-col0 tile, 32-col1 block) = 1024 pairs
+    of the ISA of search_mx_kernel (DESIGN.md s5.1 audit). NoDuplicates (KEYS 2): every unit
+    8 v_min3_u32 (half rate, the first-minimum tree) + 3.5 full-rate (its share of the
+    pair step: v_permlane32_swap, 2 v_min_u32, v_add, v_or, v_cmp per two tiles; the
+    prefetch address per four); a unit that reaches the running minimum (fraction `reach`)
+    adds the last-minimum tree: 16 v_xor + 2 integer (full) and 8 v_min3 (half). First
+    minimum only (Consistency without NoDuplicates, FK / XK keys): 8 v_min3 (half) + 1 full
+    (the frame shift). (Round 5 counted the last-minimum tree on every pair: 1 full + 1 half
+    lane-op per pair, an upper bound 2.1x the executed count at cfg2.)"""
     dupes = cfg.get("variant", 0) == 0 or cfg.get("no_dupes", False)
-    full = 1.0 if dupes else 0.0
-    half = 1.0 if dupes else 0.5
-    return 1.0 / (full / (VALU_FULL_TOPS * 1e12) + half / (VALU_HALF_TOPS * 1e12))
+    if dupes:
+        half, full = 8.0 + 8.0 * reach, 3.5 + 18.0 * reach
+    else:
+        half, full = 8.0, 1.0
+    per_unit_s = half * 64 / (VALU_HALF_TOPS * 1e12) + full * 64 / (VALU_FULL_TOPS * 1e12)
+    return 1024.0 / per_unit_s
+
+
+def mx_key_pair_peak_all_trees() -> float:
+    """The round-5 key-reduction model (both trees on every pair: 1 v_xor + 1 v_min3 per
+    pair), kept as the upper-bound view VERDICT r05 quoted (25.1 Tpairs/s)."""
+    return 1.0 / (1.0 / (VALU_FULL_TOPS * 1e12) + 1.0 / (VALU_HALF_TOPS * 1e12))
 
 
 def kernel_source_hash() -> str:
@@ -323,11 +362,11 @@ def main():
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight: step k runs on stream k %% F with its own engine, so "
                          "one frame's HBM-bound stages fill the slots the previous frame's "
-                         "search leaves idle (1 = strictly one match after another). Default: "
-                         "2 on one GPU (whole frames: cfg2 7701-7771 vs 7535-7576 Mpix/s with "
-                         "3, cfg1 11642-11979 vs 7076-9867; profiles/inflight_r02.jsonl), 6 for "
-                         "N > 1 row bands and --band-of (band 0 of 8: cfg5 0.2140-0.2146 vs "
-                         "0.2244-0.2281 ms with 3, cfg2 within 1 %%; profiles/bands_inflight_r05.jsonl)")
+                         "search leaves idle (1 = strictly one match after another). Default on "
+                         "one GPU: per config (INFLIGHT_DEFAULT: 2 for cfg1 / cfg3, else 1; "
+                         "profiles/inflight_r06.jsonl), 6 for N > 1 row bands and --band-of "
+                         "(band 0 of 8: cfg5 0.2140-0.2146 vs 0.2244-0.2281 ms with 3, cfg2 within "
+                         "1 %%; profiles/bands_inflight_r05.jsonl)")
     ap.add_argument("--no-host-path", action="store_true",
                     help="skip the end-to-end host-buffer measurement (rank 0, N=1)")
     ap.add_argument("--selftest-launch", action="store_true", help=argparse.SUPPRESS)
@@ -364,9 +403,13 @@ def main():
                          "step, on a side stream, the N-1 other bands' packed maps are written "
                          "into a root buffer: by a full-grid torch copy kernel (kernel), by "
                          "--root-load-wgs long-lived copy workgroups the way RCCL receives on the "
-                         "root's CUs (proxy: tools/ingress_proxy.hip), or by the DMA engine (dma: "
-                         "a pinned-host upload, PCIe-rate, at most one in flight). Reports the "
-                         "band's rate under that load.")
+                         "root's CUs (proxy: tools/ingress_proxy.hip), or by the copy engines (dma: "
+                         "hipMemcpyAsync kind hipMemcpyDeviceToDeviceNoCU from a second HBM buffer, "
+                         "split over --root-load-streams streams). Every form lands every step's "
+                         "bytes, with the gather pipeline's back pressure. Reports the band's rate "
+                         "under that load and the achieved ingress.")
+    ap.add_argument("--root-load-streams", type=int, default=2,
+                    help="--root-load dma: side streams the per-step copy is split over (1-4)")
     ap.add_argument("--root-load-wgs", type=int, default=16,
                     help="--root-load proxy: copy workgroups (RCCL channels x peers)")
     ap.add_argument("--root-load-high-priority", action="store_true",
@@ -453,7 +496,7 @@ def main():
     s1 = torch.from_numpy(R).to(dev)
     del L, R
     F = max(1, args.inflight if args.inflight is not None else
-            (2 if world == 1 and args.band_of == 1 else 6))
+            (inflight_default(args.config) if world == 1 and args.band_of == 1 else 6))
     # one engine (workspace) and one stream per frame in flight; slot 0 = torch's stream
     engines = [device.Engine(local_dev) for _ in range(F)]
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(F - 1)]
@@ -543,13 +586,21 @@ def main():
         bpp = (2 if (i16 or not has_corr) else 4) + (4 if has_corr else 0)
         ing = (args.band_of - 1) * band_height(H, args.band_of) * W * bpp
         ing = (ing + 15) // 16 * 16
+        nst = max(1, min(4, args.root_load_streams)) if args.root_load == "dma" else 1
         load = {"mode": args.root_load, "bytes_per_step": ing, "issued": 0, "skipped": 0,
                 "dst": torch.empty(ing // 4, dtype=torch.int32, device=dev),
-                "src": (torch.ones(ing // 4, dtype=torch.int32).pin_memory()
-                        if args.root_load == "dma" else
-                        torch.ones(ing // 4, dtype=torch.int32, device=dev)),
+                "src": torch.ones(ing // 4, dtype=torch.int32, device=dev),
                 "stream": torch.cuda.Stream(dev, priority=-1 if args.root_load_high_priority else 0),
+                "streams": [torch.cuda.Stream(dev) for _ in range(nst)],
+                "side_ev": [torch.cuda.Event() for _ in range(nst)],
                 "ev": torch.cuda.Event(), "ring": [torch.cuda.Event() for _ in range(max(2, F))]}
+        if args.root_load == "dma":
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                           ctypes.c_int, ctypes.c_void_p]
+            hip.hipMemcpyAsync.restype = ctypes.c_int
+            load["hip"] = hip
         if args.root_load == "proxy":
             import ctypes
             so = os.path.join(ROOT, "build", "ingress_proxy.so")
@@ -561,26 +612,39 @@ def main():
                                                            ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
 
     def issue_load(k):
-        # one ingress per step. The copy-kernel forms apply the gather pipeline's back pressure
-        # (a band buffer is rewritten only after the gather that read it, max(2, F) steps
-        # back, is done: step() waits on ring[k % len]); the DMA form (PCIe-rate) skips a step
-        # while the last one is busy instead
-        if load["mode"] == "dma" and load["issued"] and not load["ev"].query():
-            load["skipped"] += 1
-            return
-        with torch.cuda.stream(load["stream"]):
+        # one ingress per step, every step, with the gather pipeline's back pressure (a band
+        # buffer is rewritten only after the gather that read it, max(2, F) steps back, is
+        # done: step() waits on ring[k % len])
+        ls = load["stream"]
+        with torch.cuda.stream(ls):
             if load["mode"] == "kernel":
                 torch.bitwise_or(load["src"], 0, out=load["dst"])  # a CU kernel: read + write
             elif load["mode"] == "proxy":
                 rc = load["proxy"].ingress_proxy_launch(load["dst"].data_ptr(), load["src"].data_ptr(),
                                                         load["bytes_per_step"], args.root_load_wgs,
-                                                        load["stream"].cuda_stream)
+                                                        ls.cuda_stream)
                 if rc:
                     raise RuntimeError("ingress_proxy_launch failed: %d" % rc)
             else:
-                load["dst"].copy_(load["src"], non_blocking=True)  # hipMemcpyAsync H2D: SDMA
-            load["ev"].record(load["stream"])
-            load["ring"][k % len(load["ring"])].record(load["stream"])
+                # the copy engines (kind 1024 = hipMemcpyDeviceToDeviceNoCU: no CU blit kernel),
+                # the bytes split over the side streams, joined back on the load stream
+                nst = len(load["streams"])
+                per = (load["bytes_per_step"] // nst + 255) // 256 * 256
+                load["ev"].record(ls)
+                for i, ss in enumerate(load["streams"]):
+                    off = i * per
+                    cnt = min(per, load["bytes_per_step"] - off)
+                    if cnt <= 0:
+                        continue
+                    ss.wait_event(load["ev"])
+                    rc = load["hip"].hipMemcpyAsync(load["dst"].data_ptr() + off,
+                                                    load["src"].data_ptr() + off, cnt, 1024,
+                                                    ss.cuda_stream)
+                    if rc:
+                        raise RuntimeError("hipMemcpyAsync (root-load dma) failed: %d" % rc)
+                    load["side_ev"][i].record(ss)
+                    ls.wait_event(load["side_ev"][i])
+            load["ring"][k % len(load["ring"])].record(ls)
         load["issued"] += 1
 
     def step():
@@ -591,7 +655,7 @@ def main():
             if not gather:
                 timed_load = load is not None and state.get("timed")
                 ring = load["ring"] if timed_load else None
-                if timed_load and load["mode"] != "dma" and k - state["k0"] >= len(ring):
+                if timed_load and k - state["k0"] >= len(ring):
                     torch.cuda.current_stream(dev).wait_event(ring[k % len(ring)])
                 engines[f].match(s0, s1, mcfg, out=outs[f], corrmap=corrs[f])
                 if timed_load:
@@ -662,8 +726,13 @@ def main():
     if gather:
         if dma is not None:
             gather_info = time_dma_exchange(dist, torch, dev, rank, world, dma, streams[0], nbytes)
+            if nccl:  # the RCCL gather of the same buffers beside it (both timed)
+                gather_info["rccl_gather_alone"] = time_gather(dist, torch, dev, nccl, rank,
+                                                               sends[0], recvs[0], nbytes, world)
         else:
             gather_info = time_gather(dist, torch, dev, nccl, rank, sends[0], recvs[0], nbytes, world)
+            if want_dma and nccl:
+                gather_info["dma_exchange"] = "unavailable: the copy-engine setup failed"
         if not args.no_verify_gather:
             verify = verify_gather(args, C, dist, torch, np, dev, nccl, rank, world, eng, mcfg,
                                    step, drain, NB, recv_all, frame_disps, disp_view, corr_view,
@@ -750,15 +819,19 @@ def main():
                 "loads_issued": load["issued"], "steps_skipped": load["skipped"],
                 "ingress_GBps": round(load["bytes_per_step"] * load["issued"] / elapsed / 1e9, 1),
                 "workgroups": args.root_load_wgs if load["mode"] == "proxy" else None,
+                "copy_streams": len(load["streams"]) if load["mode"] == "dma" else None,
                 "high_priority_stream": bool(args.root_load_high_priority),
-                "back_pressure": load["mode"] != "dma",
+                "back_pressure": True,
                 "what": "rank 0's gather ingress of an N = %d run rehearsed on one GPU: the other "
                         "%d bands' packed maps written per step into a root buffer on a side "
                         "stream (%s)" % (args.band_of, args.band_of - 1,
                                          "full-grid torch copy kernel" if load["mode"] == "kernel" else
                                          "%d long-lived copy workgroups, RCCL's receive shape" %
                                          args.root_load_wgs if load["mode"] == "proxy" else
-                                         "DMA engine, pinned-host upload at PCIe rate")},
+                                         "copy engines, hipMemcpyAsync hipMemcpyDeviceToDeviceNoCU "
+                                         "from a second HBM buffer on %d streams (reads and writes "
+                                         "rank 0's HBM: twice the real ingress's HBM bytes)"
+                                         % len(load["streams"]))},
             "verify_gather": verify,
             "cpu_baseline": cpu,
             "host_path": hp,
@@ -817,8 +890,10 @@ def setup_dma_gather(args, dist, torch, dev, nccl, rank, world, recv_all, sends,
             hip.hipMemcpyAsync.restype = ctypes.c_int
 
             def copy_fn(i, stream):
+                # kind 1024 = hipMemcpyDeviceToDeviceNoCU: the copy engines, never a blit kernel
+                # on either GPU's compute units
                 rc = hip.hipMemcpyAsync(remote[i][rank].data_ptr(), sends[i].data_ptr(), nbytes,
-                                        3, stream.cuda_stream)  # hipMemcpyDeviceToDevice
+                                        1024, stream.cuda_stream)
                 if rc != 0:
                     raise RuntimeError("hipMemcpyAsync (dma gather) failed: %d" % rc)
             # self-test: a rank-specific pattern through slot 0
@@ -997,10 +1072,16 @@ def verify_gather(args, C, dist, torch, np, dev, nccl, rank, world, eng, mcfg, s
 
 def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, world,
                     ms_per_step, step_px):
-    """The dominant kernel (the Hamming search) and the HBM-bound stages, each launched
-    back to back on this rank's band and timed with HIP events on the stream they run on,
-    against their rooflines; PMC HBM bytes from profiles/ when they were
-    measured on these sources; the whole match's HBM-read fraction."""
+    """The dominant launch of the match and the HBM-bound stages, timed with HIP events on
+    the stream they run on, against their rooflines; PMC HBM bytes from
+    profiles/ when they were measured on these sources; the whole match's HBM-read fraction.
+
+    In the frame: per rep both transforms, then EXACTLY the launches
+    the match issues after its transform (bicos_search_agree_device: for cfg1 / cfg2 / cfg5
+    one fused search + agree launch, bicos_match_plan PLAN_AGREE_IN_SEARCH), with events
+    around them. Where that is one fused launch it is the line's kernel; elsewhere the search
+    alone, timed the same way, is (the stage time beside it)."""
+    from libbicos_amd import _lib, device
     st = torch.cuda.current_stream(dev)
     d0 = eng.transform(s0, mcfg.mode, words)
     d1 = eng.transform(s1, mcfg.mode, words)
@@ -1010,20 +1091,27 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     mc = C["cfg"]
     mv = mc.get("min_variance")
     mv = None if mv is None or mv < 0 else mv * n
-    from libbicos_amd import device
     ubits = device.used_bits(n, mcfg.mode)
     sbits = transform_bits(n, mcfg.mode)
+    plan = eng.plan(s0, s1, mcfg)
+    fused = bool(plan & _lib.PLAN_AGREE_IN_SEARCH)
+    thr = mc.get("nxcorr_threshold")
+    has_corr = thr is not None
+    st_out = torch.empty((rows, W), dtype=torch.float32 if has_corr else torch.int16, device=dev)
+    st_corr = torch.empty((rows, W), dtype=torch.float64 if mcfg.precision else torch.float32,
+                          device=dev) if has_corr else None
 
     def search_launch():
         # with the used-bits hint the pipeline passes (engine.cpp match_device)
         eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw, bits=ubits)
 
+    def stage_launch():  # the match past its transform (bicos_search_agree_device)
+        eng.search_agree(d0, d1, s0, s1, mcfg, out=st_out, corrmap=st_corr)
+
     reps = args.kernel_reps
-    thr = mc.get("nxcorr_threshold")
     search_launch()  # warm
-    # In the frame: the stages one after another as match_device issues them
-    # -- both transforms, the search, the agree / subpixel -- with events around the search
-    # only, so it meets the caches and clocks the frame leaves it; then back to back.
+    stage_launch()
+    # in the frame: the search alone (its own events), then the post-transform stage
     fe = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(reps)]
     for a, b in fe:
@@ -1034,6 +1122,14 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
         b.record(st)
         if thr is not None:
             eng.agree(raw, s0, s1, thr, minvar_scaled=mv, step=mc.get("subpixel_step"))
+    fs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(reps)]
+    for a, b in fs:
+        eng.transform(s0, mcfg.mode, words, out=d0)
+        eng.transform(s1, mcfg.mode, words, out=d1)
+        a.record(st)
+        stage_launch()
+        b.record(st)
     ev[0].record(st)
     for _ in range(reps):
         search_launch()
@@ -1049,8 +1145,10 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     ev[4].record(st)
     torch.cuda.synchronize(dev)
     t_b2b = ev[0].elapsed_time(ev[1]) / reps * 1e-3
-    in_frame = sorted(a.elapsed_time(b) * 1e-3 for a, b in fe)
-    t_search = sum(in_frame) / len(in_frame)  # the in-frame average: the reported figure
+    in_frame = [a.elapsed_time(b) * 1e-3 for a, b in fe]
+    t_search = sum(in_frame) / len(in_frame)  # the in-frame average
+    st_frame = [a.elapsed_time(b) * 1e-3 for a, b in fs]
+    t_stage = sum(st_frame) / len(st_frame)
     t_tf = ev[1].elapsed_time(ev[2]) / reps * 1e-3
     t_agree = ev[3].elapsed_time(ev[4]) / reps * 1e-3
     pairs = search_pairs(rows, W, mc)
@@ -1067,10 +1165,7 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     mx = mx_search()
     cons = mc.get("variant", 0) == 1
     nodupes = not cons or bool(mc.get("no_dupes", False))
-    # packed keys: the NoDuplicates search of 32/64-bit descriptors, Consistency's with
-    # no_dupes too (search_mx.hip search_pk_kernel, search_mx_geometry; ADVICE r04: the
-    # engine's own condition): the same FP4 MFMA products, two distances per register
-    pk = mx and nodupes and words <= 2
+    pk = bool(plan & _lib.PLAN_PACKED_KEYS)
     kname = ("search_pk_kernel" if pk else "search_mx_kernel") if mx else "search16_kernel"
     cfgname = args.config
     # the search stage's bytes per frame: every search dispatch (tail launches, both
@@ -1088,47 +1183,100 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
         mark = torch.zeros((rows, W + 1), dtype=torch.bool, device=dev)
         mark.scatter_(1, torch.where(ok, c0 - fwd.long(), torch.full_like(c0, W)), True)
         kept = float(mark[:, :W].sum().item())
-    # (search_mx_agree_fusable: the 128-bit shape of cfg2 / cfg5, the packed-key one of cfg1)
-    fused = bool(mx and not cons and C.get("dtype", "u8") == "u8" and not mc.get("precision")
-                 and mc.get("subpixel_step") is None and
-                 ((not pk and n == 33 and words == 4) or (pk and n == 8 and words == 1)))
+        if plan & _lib.PLAN_DENSE_ROWS:
+            # dense-row fast path: rows whose forward search kept >= 7/8 of their col0 search
+            # every col0 in the reverse pass (search_mx.hip dense_row)
+            dense = ok.sum(dim=1) * 8 >= 7 * W
+            kept = float(torch.where(dense, torch.full_like(mark[:, 0], W, dtype=torch.int64),
+                                     mark[:, :W].sum(dim=1)).sum().item())
     if mx:
         alg_flops, used_flops = mx_flops(rows, W, words, mc, ubits, sbits, reverse_col1=kept)
-        achieved_tf = alg_flops / t_search / 1e12
-        kpeak = (pk_key_pair_peak() if pk else mx_key_pair_peak(words, mc)) / 1e9
+        kpeak = (pk_key_pair_peak() if pk else mx_key_pair_peak(words, mc, mx_reach_planted(W))) / 1e9
         evaluated = pairs + (kept if kept is not None else pairs / W) * W if cons else pairs
         k_exec = int(round(alg_flops / (2 * evaluated)))
+        # the launch the line is about: the fused search + agree (the match's own launch) or
+        # the search alone
+        t_main = t_stage if fused else t_search
+        t_fp4 = alg_flops / (MFMA_FP4_DENSE_TFLOPS * 1e12)      # the matrix-core floor
+        t_key = evaluated / (kpeak * 1e9)                       # the key reduction as executed
+        t_ag = ag_bytes / (HBM_PEAK_GBS * 1e9) if fused else 0.0  # the fused agree's bytes
+        bound = "valu" if t_key > t_fp4 else "mfma"
+        t_bound = max(t_fp4, t_key) + t_ag
+        achieved_tf = alg_flops / t_main / 1e12
         fp4 = {"achieved": round(achieved_tf, 1), "peak": MFMA_FP4_DENSE_TFLOPS, "unit": "TFLOP/s",
                "frac": round(achieved_tf / MFMA_FP4_DENSE_TFLOPS, 4)}
-        kview = {"achieved": round(evaluated / t_search / 1e9, 1), "peak": round(kpeak, 1),
-                 "unit": "Gpairs/s", "frac": round(evaluated / t_search / 1e9 / kpeak, 4)}
-        kname_long = (("search_pk_kernel<%d words> x2 (forward + reverse over the kept col1) + "
-                       "consistency_kernel" if pk else
-                       "search_mx_kernel<%d words> x2 (forward + reverse FP4 MFMA Hamming argmin "
-                       "over the kept col1) + consistency_kernel") % words
-                      if cons else
-                      "search_pk_kernel<%d words> (FP4 MFMA Hamming products, two distances per "
-                      "accumulator register, v_pk_minimum3_f16 trees)" % words if pk else
-                      "search_mx_kernel<%d words> (FP4 MFMA Hamming products, argmin keys in the "
-                      "accumulator)" % words)
-        # the packed-key search is bound by its VALU key reduction (ADVICE / VERDICT r04): its
-        # line names that bound, with the FP4 view beside it; the one-product search is
-        # co-bound and reported against the dense FP4 peak
-        main = dict(kview, bound="valu") if pk else dict(fp4, bound="mfma")
+        kview = {"achieved": round(evaluated / t_main / 1e9, 1), "peak": round(kpeak, 1),
+                 "unit": "Gpairs/s", "frac": round(t_key / t_main, 4)}
+        if fused:
+            kname_long = ("search_pk_kernel<1 word, AG> (packed-key FP4 MFMA search with the NXC "
+                          "agree of its col0 in the same launch)" if pk else
+                          "search_mx_kernel<%d words, AG> (FP4 MFMA Hamming argmin with the NXC "
+                          "agree of its col0 in the same launch)" % words)
+        else:
+            kname_long = (("search_pk_kernel<%d words> x2 (forward + reverse over the kept col1)"
+                           if pk else
+                           "search_mx_kernel<%d words> x2 (forward + reverse FP4 MFMA Hamming argmin "
+                           "over the kept col1)") % words
+                          if cons else
+                          "search_pk_kernel<%d words> (FP4 MFMA Hamming products, two distances per "
+                          "accumulator register, v_pk_minimum3_f16 trees)" % words if pk else
+                          "search_mx_kernel<%d words> (FP4 MFMA Hamming products, argmin keys in the "
+                          "accumulator)" % words)
+        # frac = the launch's bound time over its measured time: max(matrix-core floor, key
+        # reduction issue as executed) + the fused agree's bytes at 8 TB/s. achieved / peak in
+        # pairs/s so that achieved / peak = frac: peak = the pairs the bound would evaluate in
+        # the launch time.
         roof = {
             "kernel": kname_long,
-            "bound": main["bound"],
-            "achieved": main["achieved"],
-            "peak": main["peak"],
-            "unit": main["unit"],
-            "frac": main["frac"],
-            "timing": "in frame: the average of %d searches timed with HIP events on their stream, "
-                      "each after both transforms and before the agree, as in a match" % reps,
-            # the headline shape (engine.cpp fuse_agree, search_mx_agree_fusable) runs the agree
-            # inside this kernel's launch in the match itself; the search is timed alone here
+            "bound": bound,
+            "achieved": round(evaluated / t_main / 1e9, 1),
+            "peak": round(evaluated / t_bound / 1e9, 1),
+            "unit": "Gpairs/s",
+            "frac": round(t_bound / t_main, 4),
+            "bound_model": {
+                "what": "max(FP4 floor, VALU key reduction as executed)%s over the launch time"
+                        % (" + the fused agree's algorithmic bytes at 8 TB/s" if fused else ""),
+                "fp4_floor_ms": round(t_fp4 * 1e3, 4),
+                "key_reduction_ms": round(t_key * 1e3, 4),
+                "agree_hbm_ms": round(t_ag * 1e3, 4),
+                "bound_ms": round(t_bound * 1e3, 4),
+                "key_model": ("pk_key_pair_peak: 10 half-rate + 1 full-rate lane-ops per lane, wide "
+                              "tile and block" if pk else
+                              "mx_key_pair_peak: the ISA's VALU per (wave, tile, block), the "
+                              "last-minimum tree weighted by the planted frame's reach fraction "
+                              "%.3f (tools/reach_sim.py); DESIGN.md s5.1" % mx_reach_planted(W)),
+            },
+            "timing": ("in frame: the average of %d launches timed with HIP events on their stream, "
+                       "each after both transforms, exactly as the match issues them "
+                       "(bicos_search_agree_device)" % reps) if fused else
+                      ("in frame: the average of %d searches timed with HIP events on their "
+                       "stream, each after both transforms and before the agree, as in a match"
+                       % reps),
+            "ms_per_launch": round(t_main * 1e3, 4),
             "agree_fused_in_match": fused,
-            "back_to_back": {"ms_per_launch": round(t_b2b * 1e3, 4),
-                             "frac": round(main["frac"] * t_search / t_b2b, 4)},
+            "plan": plan,
+            "stage_after_transform_ms": round(t_stage * 1e3, 4),
+            "search_alone_in_frame": {
+                "ms": round(t_search * 1e3, 4),
+                "fp4_frac": round(alg_flops / t_search / 1e12 / MFMA_FP4_DENSE_TFLOPS, 4),
+                "back_to_back_ms": round(t_b2b * 1e3, 4),
+                "what": "the search launch alone (bicos_search_device), a secondary view" if fused
+                        else "= this line's kernel",
+            },
+            "fp4_only_view": dict(fp4, what="the launch time against the dense FP4 MFMA peak alone "
+                                            "(2 x K FLOPs per pair)"),
+            "fp4_combined_view": {
+                "frac": round((t_fp4 + t_ag) / t_main, 4),
+                "what": "FP4 floor%s over the launch time" % (" + agree bytes at 8 TB/s" if fused else ""),
+            },
+            "key_reduction_view": dict(kview, what="the VALU key reduction as executed (issue bound "
+                                                   "at the measured rates), alone"),
+            "all_trees_view": None if pk else {
+                "peak": round(mx_key_pair_peak_all_trees() / 1e9, 1),
+                "frac": round(evaluated / mx_key_pair_peak_all_trees() / t_main, 4),
+                "what": "round 5's key-reduction model (both trees on every pair): an upper bound "
+                        "of the VALU work, 2.1x the executed count at cfg2 (DESIGN.md s5.1)",
+            },
             "reverse_col1_kept": kept,
             "traffic": traffic["bytes"],
             "traffic_source": traffic.get("source") or traffic.get("why"),
@@ -1136,21 +1284,16 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
             # algorithmic bytes
             "traffic_covers": "search + agree (one fused launch)" if fused else "search",
             "algorithmic_bytes_traffic_covers": search_bytes + ag_bytes if fused else search_bytes,
-            "algorithmic_bytes": search_bytes,
+            "algorithmic_bytes": search_bytes + (ag_bytes if fused else 0),
             "algorithmic_flops": alg_flops,
             "k_bits_per_pair": k_exec,
             "used_bits_view": {
                 "what": "the same launch time against 2 x the bits the transform sets per "
                         "descriptor (%d of %d)" % (sbits, k_exec),
                 "flops": used_flops,
-                "frac": round(used_flops / t_search / 1e12 / MFMA_FP4_DENSE_TFLOPS, 4),
+                "frac": round(used_flops / t_main / 1e12 / MFMA_FP4_DENSE_TFLOPS, 4),
             },
-            "fp4_view" if pk else "key_reduction_view": dict(
-                fp4 if pk else kview,
-                what="dense FP4 MFMA peak, 2 x K FLOPs per pair" if pk else
-                     "issue bound of the VALU key reduction, see valu_view"),
             "pairs_per_launch": evaluated,
-            "ms_per_launch": round(t_search * 1e3, 4),
             "peak_model": "dense FP4 MFMA peak (MI355X_MICROARCH.md); algorithmic FLOPs = 2 x K "
                           "per Hamming pair, K = the descriptor bits multiplied (the descriptor "
                           "width, less whole 64-bit K-steps above the set bits): never more "
@@ -1159,14 +1302,6 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
                 "peak": MFMA_FP4_SUSTAINED_TFLOPS,
                 "frac": round(achieved_tf / MFMA_FP4_SUSTAINED_TFLOPS, 4),
                 "source": "profiles/mfma_rates_r01.jsonl (tools/mfma_rate.hip, 4 waves/SIMD)",
-            },
-            "valu_view": {
-                "what": ("the VALU key reduction (packed f16 trees, pk_key_pair_peak)" if pk else
-                         "the VALU key reduction (v_min3 + v_xor per pair) that co-bounds the "
-                         "kernel") + "; issue bound at the measured rates, see DESIGN.md s5",
-                "achieved_Gpairs": round(evaluated / t_search / 1e9, 1),
-                "peak_Gpairs": round(kpeak, 1),
-                "frac": round(evaluated / t_search / 1e9 / kpeak, 4),
             },
         }
     else:

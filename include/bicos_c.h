@@ -236,6 +236,31 @@ int bicos_agree_stage_device(const int16_t* raw, const void* stack0, const void*
                              float threshold, float step, int has_minvar, float minvar_scaled,
                              int precision, float* out, void* corrmap, void* stream);
 
+/* What bicos_match_device runs for a shape and config past the descriptor transform
+ * (tests, benchmarks): a mask of BICOS_PLAN_* bits, or a negative BICOS_E_* code for an
+ * invalid configuration. stack0 / stack1 are only inspected for their alignment. No
+ * reference counterpart (its kernels are fixed per build). */
+#define BICOS_PLAN_MATRIX_CORES 1           /* the FP4 MFMA search (search_mx.hip) */
+#define BICOS_PLAN_PACKED_KEYS 2            /* its packed-key form (search_pk_kernel) */
+#define BICOS_PLAN_AGREE_IN_SEARCH 4        /* the NXC agree inside the search launch */
+#define BICOS_PLAN_REVERSE_COMPACTED 8      /* Consistency: reverse search over kept col1 */
+#define BICOS_PLAN_CONSISTENCY_IN_AGREE 16  /* Consistency: left-right check in the agree */
+#define BICOS_PLAN_DENSE_ROWS 32            /* ... rows kept >= 7/8 skip the entry prologue */
+int bicos_match_plan(bicos_engine* e, const void* stack0, const void* stack1, int n, int rows,
+                     int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                     const BicosConfig* cfg, int has_nxcorr);
+
+/* bicos_match_device from its search on: desc0 / desc1 are the two stacks' descriptors as
+ * bicos_transform_device writes them (rows x bicos_desc_pitch(cols, words) uint32, words =
+ * bicos_descriptor_words(n, cfg->mode)); the stacks are still read by the agree / subpixel
+ * stage. Exactly the launches the match issues after its transform (bicos_match_plan), so
+ * benchmarks can time them in isolation; same outputs as bicos_match_device. */
+int bicos_search_agree_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* desc1,
+                              const void* stack0, const void* stack1, int n, int rows, int cols,
+                              size_t row_pitch, size_t plane_pitch, int depth,
+                              const BicosConfig* cfg, int has_nxcorr, void* disparity,
+                              void* corrmap, void* stream);
+
 /* Build identification (arch, flags) for reports. */
 const char* bicos_build_info(void);
 

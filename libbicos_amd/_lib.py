@@ -59,7 +59,16 @@ EXPORTS = (
     "bicos_match_device", "bicos_match_device_i16", "bicos_match_host", "bicos_match_host_multi", "bicos_match_bands_device",
     "bicos_desc_pitch", "bicos_transform_device", "bicos_search_device",
     "bicos_agree_device", "bicos_subpixel_device", "bicos_agree_stage_device", "bicos_build_info",
+    "bicos_match_plan", "bicos_search_agree_device",
 )
+
+# bicos_match_plan bits (include/bicos_c.h)
+PLAN_MATRIX_CORES = 1
+PLAN_PACKED_KEYS = 2
+PLAN_AGREE_IN_SEARCH = 4
+PLAN_REVERSE_COMPACTED = 8
+PLAN_CONSISTENCY_IN_AGREE = 16
+PLAN_DENSE_ROWS = 32
 
 
 def build(verbose: bool = False, jobs: int = 4) -> str:
@@ -143,6 +152,11 @@ def lib() -> ctypes.CDLL:
     L.bicos_subpixel_device.restype = I
     L.bicos_agree_stage_device.argtypes = [P, P, P, I, I, I, Z, Z, I, F, F, I, F, I, P, P, P]
     L.bicos_agree_stage_device.restype = I
+    L.bicos_match_plan.argtypes = [P, P, P, I, I, I, Z, Z, I, ctypes.POINTER(BicosConfig), I]
+    L.bicos_match_plan.restype = I
+    L.bicos_search_agree_device.argtypes = [P, P, P, P, P, I, I, I, Z, Z, I,
+                                            ctypes.POINTER(BicosConfig), I, P, P, P]
+    L.bicos_search_agree_device.restype = I
     L.bicos_build_info.restype = ctypes.c_char_p
     L.bicos_build_info.argtypes = []
     _lib = L

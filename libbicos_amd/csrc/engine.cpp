@@ -118,6 +118,15 @@ static bool fuse_agree() {
     }();
     return on;
 }
+// Consistency's left-right check inside the agree launch (kernels.hip agree_lds_kernel CONS;
+// BICOS_FUSE_CONS=0: consistency_kernel + the agree; read once)
+static bool fuse_consistency() {
+    static const bool on = [] {
+        const char* v = std::getenv("BICOS_FUSE_CONS");
+        return !(v && !std::strcmp(v, "0"));
+    }();
+    return on;
+}
 
 // Search implementation: the matrix-core search (search_mx.hip) unless the engine is tuned
 // to the VALU search (bicos_engine_tune variant 16) or BICOS_SEARCH=valu;
@@ -180,6 +189,19 @@ static bool reverse_compacted(bool mx) {
     return mx && !full;
 }
 
+// Consistency's dense-row fast path (SearchArgs.row_valid, search_mx.hip dense_row): the
+// forward search counts its valid col0 per 32-column tile and the compacted reverse search
+// skips its entry prologue on rows that kept >= 7/8 of them. BICOS_DENSE_ROWS=0: off (A/B).
+static bool dense_rows() {
+    static const bool on = [] {
+        const char* v = std::getenv("BICOS_DENSE_ROWS");
+        return !(v && !std::strcmp(v, "0"));
+    }();
+    return on;
+}
+// bytes per row of the per-tile valid counts
+static size_t valid_pitch(int cols) { return ((size_t)(cols + 31) / 32 + 15) / 16 * 16; }
+
 // Bytes the kernels may address from a stack base; the kernels use 32-bit buffer offsets.
 static int stack_span(int n, int rows, int cols, size_t row_pitch, size_t plane_pitch, int depth,
                       uint32_t* out) {
@@ -195,10 +217,46 @@ static int stack_span(int n, int rows, int cols, size_t row_pitch, size_t plane_
     return BICOS_OK;
 }
 
+// What match_device runs for a shape and config (bicos_match_plan's bits, bicos_c.h): the
+// kernels after the transform. Valid configurations only (match_device validates first).
+int match_plan(const bicos_engine* e, int n, int rows, int cols, size_t row_pitch,
+               size_t plane_pitch, int depth, const BicosConfig& cfg, bool has_nxcorr,
+               const void* s0, const void* s1) {
+    const int mode = cfg.mode == 0 ? 0 : 1;
+    const int words = descriptor_words(n, mode);
+    if (words < 0 || rows <= 0 || cols <= 0) return 0;
+    const bool consistency = cfg.variant_type != 0;
+    const bool nodupes = consistency ? cfg.no_dupes != 0 : true;
+    const bool has_step = has_nxcorr && cfg.subpixel_step >= 0;
+    const bool dbl = cfg.precision != 0;
+    const bool mx = use_mx(e);
+    // the LDS-staged agree kernels read the left planes with dword loads
+    const bool aligned4 = ((row_pitch * depth | plane_pitch * depth) & 3) == 0 &&
+                          (((uintptr_t)s0 | (uintptr_t)s1) & 3) == 0;
+    int plan = 0;
+    if (mx) {
+        plan |= BICOS_PLAN_MATRIX_CORES;
+        const bicos_hip::MxGeometry g = mx_geometry(e, rows, cols, words, used_bits(n, mode));
+        if (g.pk && nodupes) plan |= BICOS_PLAN_PACKED_KEYS;
+        if (!consistency && has_nxcorr && !has_step && aligned4 && fuse_agree() &&
+            bicos_hip::search_mx_agree_fusable(g, words, true, cols, n, depth, dbl))
+            plan |= BICOS_PLAN_AGREE_IN_SEARCH;
+    }
+    if (consistency) {
+        if (reverse_compacted(mx)) {
+            plan |= BICOS_PLAN_REVERSE_COMPACTED;
+            if (dense_rows()) plan |= BICOS_PLAN_DENSE_ROWS;
+        }
+        if (has_nxcorr && !has_step && aligned4 && n <= 65 && fuse_consistency())
+            plan |= BICOS_PLAN_CONSISTENCY_IN_AGREE;
+    }
+    return plan;
+}
+
 int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int rows, int cols,
                  size_t row_pitch, size_t plane_pitch, int depth, const BicosConfig& cfg,
                  bool has_nxcorr, float threshold, void* disp, void* corr, hipStream_t st,
-                 bool disp_i16) {
+                 bool disp_i16, const uint32_t* ext_d0, const uint32_t* ext_d1) {
     if (!e) return fail(BICOS_E_ARG, "null engine");
     if (n < 2) return fail(BICOS_E_ARG, "need at least two images");
     if (depth != 1 && depth != 2)
@@ -234,11 +292,18 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
 
     const bool mx = use_mx(e);
 
-    // workspace: desc0 | desc1 | raw int16 | fwd | rev (Consistency)
+    const int plan = match_plan(e, n, rows, cols, row_pitch, plane_pitch, depth, cfg, has_nxcorr,
+                                s0, s1);
+    // workspace: desc0 | desc1 | raw int16 | fwd | rev (Consistency); the descriptors are the
+    // caller's when given (bicos_search_agree_device: the match past its transform)
     const size_t dpitch = bicos_desc_pitch(cols, words);
-    const size_t desc_bytes = align_up((size_t)rows * dpitch * 4);
+    const bool ext = ext_d0 != nullptr;
+    if (ext != (ext_d1 != nullptr)) return fail(BICOS_E_ARG, "need both descriptor buffers");
+    const size_t desc_bytes = ext ? 0 : align_up((size_t)rows * dpitch * 4);
     const size_t map16 = align_up((size_t)rows * cols * 2);
-    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) + (consistency ? 2 * map16 : 0);
+    const size_t vpitch = valid_pitch(cols);
+    const size_t vbytes = (plan & BICOS_PLAN_DENSE_ROWS) ? align_up((size_t)rows * vpitch) : 0;
+    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) + (consistency ? 2 * map16 : 0) + vbytes;
     int rc = reserve(e->ws, e->ws_bytes, need, e->device, st, e->ws_ready);
     if (rc) return rc;
     // order against earlier users of ws / stage on other streams; mark our use on exit
@@ -250,28 +315,35 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
         ~MarkUse() { (void)hipEventRecord(ev, st); }
     } mark{e->ws_ready, st};
     char* p = (char*)e->ws;
-    uint32_t* d0 = (uint32_t*)p;
+    const uint32_t* d0 = ext ? ext_d0 : (const uint32_t*)p;
     p += desc_bytes;
-    uint32_t* d1 = (uint32_t*)p;
+    const uint32_t* d1 = ext ? ext_d1 : (const uint32_t*)p;
     p += desc_bytes;
     int16_t* raw = has_nxcorr ? (int16_t*)p : (int16_t*)disp;
     if (has_nxcorr) p += map16;
     int16_t* fwd = consistency ? (int16_t*)p : nullptr;
     int16_t* rev = consistency ? (int16_t*)(p + map16) : nullptr;
+    uint8_t* valid = vbytes ? (uint8_t*)(p + 2 * map16) : nullptr;  // dense-row fast path
 
     // 1. descriptor_transform, both stacks in one launch (cpu.cpp:50-59)
-    bicos_hip::TransformArgs ta{s0, s1, d0, d1, n, rows, cols, row_pitch, plane_pitch, dpitch, 0, span};
-    rc = check_hip(bicos_hip::launch_transform(ta, depth, mode, words, st), "transform launch");
-    if (rc) return rc;
+    if (!ext) {
+        bicos_hip::TransformArgs ta{s0, s1, (uint32_t*)d0, (uint32_t*)d1, n, rows, cols,
+                                    row_pitch, plane_pitch, dpitch, 0, span};
+        rc = check_hip(bicos_hip::launch_transform(ta, depth, mode, words, st), "transform launch");
+        if (rc) return rc;
+    }
 
     // 2. bicos search (cpu.cpp:68-75): NoDuplicates in one search; Consistency as the
     // forward and the reverse search (the same search with the stacks swapped, bicos.hpp:96)
     // over only the col1 the forward search kept (reverse_search), then the left-right check
     auto search = [&](const uint32_t* a0, const uint32_t* a1, int16_t* out, int out_mode,
-                      bool nd, const char* what, const int16_t* keep = nullptr) {
+                      bool nd, const char* what, const int16_t* keep = nullptr,
+                      uint8_t* row_valid = nullptr) {
         bicos_hip::SearchArgs sa{a0, a1, out, rows, cols, dpitch, (size_t)cols, out_mode, 0, 0, 0};
         sa.keep = keep;
         sa.keep_pitch = (size_t)cols;
+        sa.row_valid = row_valid;
+        sa.valid_pitch = vpitch;
         if (mx)
             return check_hip(bicos_hip::launch_search_mx(
                                  sa, mx_geometry(e, rows, cols, words, used_bits(n, mode)), words, nd, st),
@@ -302,26 +374,28 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
 
     // the headline shape runs the agree inside the search's workgroups (one launch,
     // search_mx.hip fused_agree; BICOS_FUSE_AGREE=0 keeps the two launches)
-    const bool aligned4 = ((row_pitch | plane_pitch) & 3) == 0 &&
-                          (((uintptr_t)s0 | (uintptr_t)s1) & 3) == 0;
-    if (!consistency && has_nxcorr && !has_step && mx && aligned4 && fuse_agree()) {
+    if (plan & BICOS_PLAN_AGREE_IN_SEARCH) {
         const bicos_hip::MxGeometry g = mx_geometry(e, rows, cols, words, used_bits(n, mode));
-        if (bicos_hip::search_mx_agree_fusable(g, words, true, cols, n, depth, dbl)) {
-            bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0, 0};
-            sa.ag = aa;
-            return check_hip(bicos_hip::launch_search_mx_agree(sa, g, st), "search + agree launch");
-        }
+        bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0, 0};
+        return check_hip(bicos_hip::launch_search_mx_agree(sa, aa, g, st), "search + agree launch");
     }
 
     if (!consistency) {
         rc = search(d0, d1, raw, 0, true, "search launch");
         if (rc) return rc;
     } else {
-        rc = search(d0, d1, fwd, 1, nodupes, "search launch");
+        rc = search(d0, d1, fwd, 1, nodupes, "search launch", nullptr, valid);
         if (!rc)
             rc = search(d1, d0, rev, 1, nodupes, "reverse search launch",
-                        reverse_compacted(mx) ? fwd : nullptr);
+                        (plan & BICOS_PLAN_REVERSE_COMPACTED) ? fwd : nullptr, valid);
         if (rc) return rc;
+        if (plan & BICOS_PLAN_CONSISTENCY_IN_AGREE) {
+            // the left-right check runs inside the agree (kernels.hip agree_lds_kernel CONS)
+            aa.fwd = fwd;
+            aa.rev = rev;
+            aa.max_lr_diff = cfg.max_lr_diff;
+            return check_hip(bicos_hip::launch_agree(aa, depth, dbl, st), "consistency + agree launch");
+        }
         bicos_hip::ConsistencyArgs ca{fwd, rev, raw, rows, cols, (size_t)cols, cfg.max_lr_diff};
         rc = check_hip(bicos_hip::launch_consistency(ca, st), "consistency launch");
         if (rc) return rc;
@@ -454,6 +528,41 @@ int match_host(bicos_engine* e, const void* const* p0, const size_t* steps0,
         e->pool.reset(new HostPool((int)std::max(1u, std::min(cap, hw ? hw : 1u))));
     }
 
+    // The maps: band by band on dl_stream into pinned memory as each band's match ends,
+    // overlapping the later bands' uploads (round 6, VERDICT r05 #8: the round-5 band-wise
+    // download shared the upload stream's copy engine), then into the caller's buffers by the
+    // pool. BICOS_HOST_DL=once: one download of each map at the end (round 5).
+    static const bool dl_bands = [] {
+        const char* v = std::getenv("BICOS_HOST_DL");
+        return !(v && !std::strcmp(v, "once"));
+    }();
+    const size_t corr_bytes = corr ? (size_t)rows * cols * csz : 0;
+    if (dl_bands) {
+        if (!e->dl_stream) {
+            rc = check_hip(hipStreamCreateWithFlags(&e->dl_stream, hipStreamNonBlocking),
+                           "hipStreamCreate");
+            if (rc) return rc;
+        }
+        const size_t need_out = align_up(disp_bytes) + corr_bytes;
+        if (e->pinned_out_bytes < need_out) {
+            if (e->pinned_out) (void)hipHostFree(e->pinned_out);
+            e->pinned_out = nullptr;
+            e->pinned_out_bytes = 0;
+            rc = check_hip(hipHostMalloc(&e->pinned_out, need_out, hipHostMallocDefault),
+                           "hipHostMalloc(map staging)");
+            if (rc) return rc;
+            e->pinned_out_bytes = need_out;
+        }
+        while ((int)e->dl_events.size() < 2 * B) {
+            hipEvent_t ev;
+            rc = check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+            if (rc) return rc;
+            e->dl_events.push_back(ev);
+        }
+    }
+    char* hout_d = dl_bands ? (char*)e->pinned_out : nullptr;
+    char* hout_c = dl_bands && corr ? (char*)e->pinned_out + align_up(disp_bytes) : nullptr;
+
     // BICOS_HOST_TRACE=1: per-phase host timestamps on stderr (tools/host_bench.py)
     static const bool trace = std::getenv("BICOS_HOST_TRACE") != nullptr;
     const auto t_start = std::chrono::steady_clock::now();
@@ -517,23 +626,59 @@ int match_host(bicos_engine* e, const void* const* p0, const size_t* steps0,
                               (size_t)br * cols, depth, cfg, has_nxcorr, threshold,
                               dev_disp + (size_t)r0 * cols * dsz,
                               dev_corr ? dev_corr + (size_t)r0 * cols * csz : nullptr, cs);
+        if (!rc && dl_bands) {  // this band's rows of the maps, as soon as they are matched
+            hipStream_t ds = e->dl_stream;
+            const size_t od = (size_t)r0 * cols * dsz, oc = (size_t)r0 * cols * csz;
+            rc = check_hip(hipEventRecord(e->dl_events[2 * b], cs), "hipEventRecord");
+            if (!rc) rc = check_hip(hipStreamWaitEvent(ds, e->dl_events[2 * b], 0), "hipStreamWaitEvent");
+            if (!rc)
+                rc = check_hip(hipMemcpyAsync(hout_d + od, dev_disp + od, (size_t)br * cols * dsz,
+                                              hipMemcpyDeviceToHost, ds), "download");
+            if (!rc && corr)
+                rc = check_hip(hipMemcpyAsync(hout_c + oc, dev_corr + oc, (size_t)br * cols * csz,
+                                              hipMemcpyDeviceToHost, ds), "download");
+            if (!rc) rc = check_hip(hipEventRecord(e->dl_events[2 * b + 1], ds), "hipEventRecord");
+        }
     }
     stamp("bands queued", B);
     if (trace) {
         (void)hipStreamSynchronize(cs);
         stamp("bands matched", B);
     }
-    if (!rc) {
+    if (!rc && dl_bands) {
+        // each band into the caller's buffers as it lands (the pool: row chunks of both maps)
+        for (int b = 0; b < B && !rc; ++b) {
+            rc = check_hip(hipEventSynchronize(e->dl_events[2 * b + 1]), "hipEventSynchronize");
+            if (rc) break;
+            const int r0 = b * band_rows;
+            const int br = std::min(band_rows, rows - r0);
+            const int parts = 8;
+            const std::function<void(int)> out = [&](int i) {
+                const bool c = i >= parts;
+                if (c && !corr) return;
+                const size_t esz = c ? csz : dsz;
+                const size_t bytes = (size_t)br * cols * esz;
+                const size_t chunk = (bytes / parts + 63) / 64 * 64;
+                const size_t o = (size_t)(i % parts) * chunk;
+                if (o >= bytes) return;
+                const size_t base = (size_t)r0 * cols * esz + o;
+                std::memcpy((char*)(c ? corr : disp) + base, (c ? hout_c : hout_d) + base,
+                            std::min(chunk, bytes - o));
+            };
+            e->pool->run(2 * parts, out);
+        }
+    } else if (!rc) {
         rc = check_hip(hipMemcpyAsync(disp, dev_disp, disp_bytes, hipMemcpyDeviceToHost, cs),
                        "download");
         if (!rc && corr)
-            rc = check_hip(hipMemcpyAsync(corr, dev_corr, (size_t)rows * cols * csz,
-                                          hipMemcpyDeviceToHost, cs),
+            rc = check_hip(hipMemcpyAsync(corr, dev_corr, corr_bytes, hipMemcpyDeviceToHost, cs),
                            "download");
     }
-    // drain both streams whatever happened: the slots and the stage are reused next call
+    // drain every stream whatever happened: the slots and the stage are reused next call
     const int r1 = check_hip(hipStreamSynchronize(ks), "hipStreamSynchronize");
     const int r2 = check_hip(hipStreamSynchronize(cs), "hipStreamSynchronize");
+    const int r3 = dl_bands ? check_hip(hipStreamSynchronize(e->dl_stream), "hipStreamSynchronize")
+                            : BICOS_OK;
     stamp("downloaded", B);
     for (size_t i = 0; i < dma_ev.size(); ++i) {
         float ms = 0.f;
@@ -543,7 +688,7 @@ int match_host(bicos_engine* e, const void* const* p0, const size_t* steps0,
         (void)hipEventDestroy(dma_ev[i].first);
         (void)hipEventDestroy(dma_ev[i].second);
     }
-    return rc ? rc : (r1 ? r1 : r2);
+    return rc ? rc : (r1 ? r1 : (r2 ? r2 : r3));
 }
 
 namespace {
@@ -636,6 +781,11 @@ void bicos_engine_destroy(bicos_engine* e) {
     (void)hipStreamSynchronize(e->own_stream);
     if (e->pinned) (void)hipHostFree(e->pinned);
     for (hipEvent_t ev : e->events) (void)hipEventDestroy(ev);
+    if (e->gather_pinned) (void)hipHostFree(e->gather_pinned);
+    for (hipEvent_t ev : e->gather_events) (void)hipEventDestroy(ev);
+    if (e->pinned_out) (void)hipHostFree(e->pinned_out);
+    for (hipEvent_t ev : e->dl_events) (void)hipEventDestroy(ev);
+    if (e->dl_stream) (void)hipStreamDestroy(e->dl_stream);
     e->pool.reset();
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);
@@ -730,6 +880,38 @@ int bicos_match_device_i16(bicos_engine* e, const void* stack0, const void* stac
                               has_nxcorr, disparity, corrmap, stream, true);
 }
 
+int bicos_match_plan(bicos_engine* e, const void* stack0, const void* stack1, int n, int rows,
+                     int cols, size_t row_pitch, size_t plane_pitch, int depth,
+                     const BicosConfig* cfg, int has_nxcorr) {
+    if (!cfg) return fail(BICOS_E_ARG, "null config");
+    if (n < 2) return fail(BICOS_E_ARG, "need at least two images");
+    if (depth != 1 && depth != 2) return fail(BICOS_E_ARG, "bad input depth");
+    if (descriptor_words(n, cfg->mode ? 1 : 0) < 0) return fail(BICOS_E_BITS, "input stacks too large");
+    return match_plan(e, n, rows, cols, row_pitch, plane_pitch, depth, *cfg, has_nxcorr != 0,
+                      stack0, stack1);
+}
+
+int bicos_search_agree_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* desc1,
+                              const void* stack0, const void* stack1, int n, int rows, int cols,
+                              size_t row_pitch, size_t plane_pitch, int depth,
+                              const BicosConfig* cfg, int has_nxcorr, void* disparity,
+                              void* corrmap, void* stream) {
+    if (!cfg) return fail(BICOS_E_ARG, "null config");
+    if (!e) return fail(BICOS_E_ARG, "null engine");
+    if (rows > 0 && cols > 0 && (!desc0 || !desc1)) return fail(BICOS_E_ARG, "null descriptors");
+    try {
+        std::lock_guard<std::mutex> g(e->lock);
+        const float thr = cfg->nxcorr_threshold >= 0 ? cfg->nxcorr_threshold : 0.5f;
+        return match_device(e, stack0, stack1, n, rows, cols, row_pitch, plane_pitch, depth, *cfg,
+                            has_nxcorr != 0, thr, disparity, corrmap, (hipStream_t)stream, false,
+                            desc0, desc1);
+    } catch (const std::exception& ex) {
+        return fail(BICOS_E_INTERNAL, ex.what());
+    } catch (...) {
+        return fail(BICOS_E_INTERNAL, "unknown exception");
+    }
+}
+
 int bicos_match_host(bicos_engine* e, const void* const* stack0, const void* const* stack1, int n,
                      int rows, int cols, size_t step, int depth, const BicosConfig* cfg,
                      int has_nxcorr, void* disparity, void* corrmap) {
@@ -797,7 +979,10 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     if (!e) return fail(BICOS_E_ARG, "consistency search needs an engine workspace");
     std::lock_guard<std::mutex> lk(e->lock);  // the workspace may be shared (default engine)
     const size_t map16 = align_up((size_t)rows * cols * 2);
-    int rc = reserve(e->ws, e->ws_bytes, 2 * map16, e->device, st, e->ws_ready);
+    const bool dense = mx && reverse_compacted(true) && dense_rows();
+    const size_t vpitch = valid_pitch(cols);
+    const size_t vbytes = dense ? align_up((size_t)rows * vpitch) : 0;
+    int rc = reserve(e->ws, e->ws_bytes, 2 * map16 + vbytes, e->device, st, e->ws_ready);
     if (rc) return rc;
     rc = check_hip(hipStreamWaitEvent(st, e->ws_ready, 0), "hipStreamWaitEvent");
     if (rc) return rc;
@@ -808,10 +993,13 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
     } mark{e->ws_ready, st};
     int16_t* fwd = (int16_t*)e->ws;
     int16_t* rev = (int16_t*)((char*)e->ws + map16);
+    uint8_t* valid = dense ? (uint8_t*)e->ws + 2 * map16 : nullptr;
     bicos_hip::SearchArgs fa{desc0, desc1, fwd, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
     bicos_hip::SearchArgs ra{desc1, desc0, rev, rows, cols, dpitch, (size_t)cols, 1, 0, 0};
     if (mx) {
         const bicos_hip::MxGeometry gm = mx_geometry(e, rows, cols, words, bits);
+        fa.row_valid = ra.row_valid = valid;
+        fa.valid_pitch = ra.valid_pitch = vpitch;
         rc = check_hip(bicos_hip::launch_search_mx(fa, gm, words, nodupes, st), "search launch");
         if (rc) return rc;
         if (reverse_compacted(true)) {

@@ -65,6 +65,19 @@ struct bicos_engine {
     size_t pinned_bytes = 0;
     std::vector<hipEvent_t> events;
     std::unique_ptr<bicos_impl::HostPool> pool;
+    // host-staged multi-GPU gather (multi.cpp bicos_match_bands_device): its own pinned
+    // buffer and events, grown only (sharing match_host's slots reallocated the
+    // pinned memory whenever the two paths alternated)
+    void* gather_pinned = nullptr;
+    size_t gather_pinned_bytes = 0;
+    std::vector<hipEvent_t> gather_events;
+    // host-buffer pipeline, maps downloaded band by band on their own stream (so a copy
+    // engine other than the uploads' can take them: PCIe is full duplex) into pinned memory,
+    // then copied into the caller's buffers by the pool; 2 events per band (matched, landed)
+    hipStream_t dl_stream = nullptr;
+    void* pinned_out = nullptr;
+    size_t pinned_out_bytes = 0;
+    std::vector<hipEvent_t> dl_events;
 };
 
 namespace bicos_impl {
@@ -91,10 +104,18 @@ bicos_hip::SearchGeometry geometry(const bicos_engine* e, int rows, int cols, in
 
 // Full match on device buffers (validated arguments). corr may be null. disp_i16: the
 // disparity map is int16 even with the NXC stage (no subpixel; bicos_match_device_i16).
+// ext_d0 / ext_d1: the two stacks' descriptors (transform output, bicos_desc_pitch rows)
+// already computed -- the match then runs from its search on (bicos_search_agree_device).
 int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int rows, int cols,
                  size_t row_pitch, size_t plane_pitch, int depth, const BicosConfig& cfg,
                  bool has_nxcorr, float threshold, void* disp, void* corr, hipStream_t st,
-                 bool disp_i16 = false);
+                 bool disp_i16 = false, const uint32_t* ext_d0 = nullptr,
+                 const uint32_t* ext_d1 = nullptr);
+
+// BICOS_PLAN_* bits of what match_device runs after the transform (bicos_match_plan)
+int match_plan(const bicos_engine* e, int n, int rows, int cols, size_t row_pitch,
+               size_t plane_pitch, int depth, const BicosConfig& cfg, bool has_nxcorr,
+               const void* s0, const void* s1);
 
 // Host buffers in and out (the reference's cv::Mat path, src/impl/cpu.cpp:100-159): the
 // stacks are uploaded in row bands through pinned slots on a copy stream while earlier

@@ -568,7 +568,13 @@ __global__ __launch_bounds__(256) void agree_reg_kernel(AgreeArgs a) {
 // right gathers are all in flight together. Requires 4-byte aligned stacks, row and
 // plane pitches (checked on the host; agree_reg_kernel otherwise). Same contract and
 // results as agree_reg_kernel.
-template <typename TIn, typename TPrec, int MAXN, bool EXACT>
+//
+// CONS: Consistency's left-right check (consistency_kernel, reference bicos.hpp:99-106) in
+// the same launch -- the pixel's disparity comes from the forward / reverse search results
+// (a.fwd, a.rev) instead of a.raw: one launch and one int16 map round trip fewer per frame
+// (cfg4). The forward result and the reverse gather at it are loaded first, then the left
+// tile, so the right gathers wait on both search results but not on the tile.
+template <typename TIn, typename TPrec, int MAXN, bool EXACT, bool CONS = false>
 __global__ __launch_bounds__(256) void agree_lds_kernel(AgreeArgs a) {
     constexpr int DW = 64 * (int)sizeof(TIn);  // dwords per plane of a 256-column tile
     constexpr int WPP = 256 / DW;              // planes per pass of the workgroup
@@ -582,7 +588,17 @@ __global__ __launch_bounds__(256) void agree_lds_kernel(AgreeArgs a) {
     const int n = EXACT ? MAXN : a.n;
     const uint32_t pp = (uint32_t)a.plane_pitch;
     const uint32_t rowoff = (uint32_t)row * (uint32_t)a.row_pitch;
-    int d = live ? (int)a.raw[(size_t)row * a.raw_pitch + col] : INVALID_I16;
+    int d = INVALID_I16;
+    if constexpr (CONS) {
+        // unguarded loads (see below): an invalid or dead pixel reads column 0
+        const size_t ro = (size_t)row * a.cols;
+        const int f = a.fwd[ro + (live ? col : 0)];
+        const int rv = a.rev[ro + (f >= 0 ? f : 0)];
+        if (live && f >= 0 && rv >= 0 && abs(col - rv) <= a.max_lr_diff)
+            d = (int)(int16_t)((col + rv) / 2 - f);
+    } else {
+        d = live ? (int)a.raw[(size_t)row * a.raw_pitch + col] : INVALID_I16;
+    }
     // the range covers whole dwords: with a padded pitch and cols % 4 != 0 the stack's last
     // pixel shares a dword with up to 3 bytes past it, and a dword reaching past
     // num_records reads as 0 -- the last row's last pixels of plane n-1 came in as 0
@@ -750,6 +766,11 @@ hipError_t launch_agree_m(const AgreeArgs& a, hipStream_t st) {
     const size_t sz = sizeof(TIn);
     const bool aligned = ((uintptr_t)a.stack0 % 4 == 0) && (a.row_pitch * sz) % 4 == 0 &&
                          (a.plane_pitch * sz) % 4 == 0;
+    if (a.fwd) {  // Consistency's check in the agree: the LDS kernel only (engine.cpp plan)
+        if (!aligned || !a.rev) return hipErrorInvalidValue;
+        hipLaunchKernelGGL((agree_lds_kernel<TIn, TPrec, MAXN, false, true>), grid, dim3(256), 0, st, a);
+        return hipGetLastError();
+    }
     if (aligned) {
         // runtime n even for an exact bucket: with a constant n the compiler front-loads
         // the conversions and doubles the VGPRs (49 -> 100 at n = 33)
@@ -774,6 +795,7 @@ hipError_t launch_agree_t(const AgreeArgs& a, hipStream_t st) {
     if (n <= 48) return launch_agree_m<TIn, TPrec, 48>(a, st);
     if (n <= 65) return launch_agree_m<TIn, TPrec, 65>(a, st);
     // beyond the descriptor limit only the stage API can get here: generic kernel
+    if (a.fwd) return hipErrorInvalidValue;
     dim3 grid((a.cols + 255) / 256, a.rows);
     hipLaunchKernelGGL((agree_kernel<TIn, TPrec>), grid, dim3(256), 0, st, a);
     return hipGetLastError();

@@ -37,6 +37,13 @@ struct AgreeArgs {
     int out_f32;            // agree: 1 -> float32 output, 0 -> int16 in place semantics
     void* corrmap;          // dense [rows][cols] float (double for DOUBLE) or nullptr
     uint32_t stack_bytes;   // bytes addressable from each stack base (< 4 GiB)
+    // Consistency's left-right check inside the agree (launch_agree with fwd != nullptr,
+    // aligned stacks): the disparity of pixel (row, col) is consistency_kernel's -- fwd[col]
+    // the forward search's best col1 (or -1), rev[col1] the reverse search's best col0 (or
+    // -1), both dense [rows][cols] -- instead of raw[col] (reference bicos.hpp:99-106)
+    const int16_t* fwd;
+    const int16_t* rev;
+    int max_lr_diff;
 };
 
 struct SearchArgs {
@@ -58,8 +65,21 @@ struct SearchArgs {
     // (keep = the forward result, best col1 or -1; reference bicos.hpp:94-101)
     const int16_t* keep;
     size_t keep_pitch;      // int16 elements
-    // launch_search_mx_agree only: the agree stage (ag.raw unused) run by each workgroup over
-    // its own col0 once their search is done
+    // Consistency's dense-row fast path (launch_search_mx only; nullptr: off). The forward
+    // search (out_mode 1, keep == nullptr) writes, per row and 32-col0 tile c0 / 32, how many
+    // of its col0 found a valid match (u8, row stride valid_pitch bytes >= ceil(cols / 32)).
+    // The compacted reverse search (keep != nullptr) reads its row's counts first: a row
+    // whose forward search kept >= 7/8 of its col0 skips the entry prologue and searches
+    // every col0 of the row (a superset of the kept col1: the check reads rev only there).
+    uint8_t* row_valid;
+    size_t valid_pitch;
+};
+
+// launch_search_mx_agree: the search and the agree stage (ag.raw unused) that each workgroup
+// runs over its own col0 once their search is done. Only those kernel instantiations take
+// the agree's arguments (every other search launch keeps the small SearchArgs)
+struct SearchAgreeArgs {
+    SearchArgs s;
     AgreeArgs ag;
 };
 
@@ -130,7 +150,8 @@ hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool n
 // of n = 8; float, no subpixel step. search_mx_agree_fusable says whether g / the match are one.
 bool search_mx_agree_fusable(const MxGeometry& g, int words, bool nodupes, int cols, int n,
                              int depth, bool dbl);
-hipError_t launch_search_mx_agree(SearchArgs a, const MxGeometry& g, hipStream_t st);
+hipError_t launch_search_mx_agree(SearchArgs a, const AgreeArgs& ag, const MxGeometry& g,
+                                  hipStream_t st);
 hipError_t launch_agree(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
 hipError_t launch_subpixel(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
 // n > 40 (subpixel_wide.hip); launch_subpixel dispatches to it

@@ -249,18 +249,18 @@ extern "C" int bicos_match_bands_device(const int* devices, int ndev, const void
             if (!rc && !direct[e->device]) {
                 // the host-staged gather: the stage layout mirrored in this engine's pinned
                 // buffer, one event per band for the root's stream to wait on
-                if (e->pinned_bytes < kv.second) {
-                    if (e->pinned) (void)hipHostFree(e->pinned);
-                    e->pinned = nullptr;
-                    e->pinned_bytes = 0;
-                    rc = check_hip(hipHostMalloc(&e->pinned, kv.second, hipHostMallocDefault),
+                if (e->gather_pinned_bytes < kv.second) {
+                    if (e->gather_pinned) (void)hipHostFree(e->gather_pinned);
+                    e->gather_pinned = nullptr;
+                    e->gather_pinned_bytes = 0;
+                    rc = check_hip(hipHostMalloc(&e->gather_pinned, kv.second, hipHostMallocDefault),
                                    "hipHostMalloc(gather staging)");
-                    if (!rc) e->pinned_bytes = kv.second;
+                    if (!rc) e->gather_pinned_bytes = kv.second;
                 }
-                while (!rc && (int)e->events.size() < copies[e->device]) {
+                while (!rc && (int)e->gather_events.size() < copies[e->device]) {
                     hipEvent_t ev;
                     rc = check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
-                    if (!rc) e->events.push_back(ev);
+                    if (!rc) e->gather_events.push_back(ev);
                 }
             }
             if (rc) {
@@ -308,9 +308,9 @@ extern "C" int bicos_match_bands_device(const int* devices, int ndev, const void
                 continue;
             }
             // host-staged: down on the band's stream, up on the root's once that is done
-            char* hd = (char*)e->pinned + od;
-            char* hc = corrmap ? (char*)e->pinned + oc : nullptr;
-            hipEvent_t ev = e->events[ev_used[e->device]++];
+            char* hd = (char*)e->gather_pinned + od;
+            char* hc = corrmap ? (char*)e->gather_pinned + oc : nullptr;
+            hipEvent_t ev = e->gather_events[ev_used[e->device]++];
             if (!rc) rc = check_hip(hipMemcpyAsync(hd, sd, bd, hipMemcpyDeviceToHost, e->own_stream), "gather (download)");
             if (!rc && corrmap)
                 rc = check_hip(hipMemcpyAsync(hc, sc, bc, hipMemcpyDeviceToHost, e->own_stream), "gather (download)");

@@ -356,6 +356,34 @@ inline int list_grid(int rows, int tiles_per_row) {
     return 8 * ((r8 + LIST_GROUP - 1) / LIST_GROUP) * LIST_GROUP * tiles_per_row;
 }
 
+// Consistency's dense-row fast path (SearchArgs.row_valid): the compacted reverse search's
+// workgroup sums its row's per-tile valid counts, written by the forward search's epilogue
+// (tile_valid_store), in every wave -- a workgroup-uniform answer without a barrier. A row
+// whose forward search kept >= 7/8 of its col0 skips list_prologue (one dependent read of
+// the whole forward row, an LDS bitmap and a scan: ~9 us per cfg4 frame, where 98 % of the
+// columns are kept) and searches its col0 in order -- every rev the check could read is
+// then computed, plus a few it does not read.
+__device__ __forceinline__ bool dense_row(const SearchArgs& a, int row) {
+    const uint8_t* v = a.row_valid + (size_t)row * a.valid_pitch;
+    const int nt = (a.cols + 31) >> 5;
+    const int lane = threadIdx.x & 63;
+    int sum = 0;
+    for (int i = lane; i < nt; i += 64) sum += v[i];
+#pragma unroll
+    for (int sh = 32; sh >= 1; sh >>= 1) sum += __shfl_xor(sum, sh);
+    return __builtin_amdgcn_readfirstlane(sum) * 8 >= 7 * a.cols;
+}
+// forward search epilogue, dense-row fast path: the valid results of one 32-col0 tile (the
+// 32 lanes of this lane's half-wave, lane & 31 = col0 % 32) counted into
+// row_valid[row][c0_tile / 32] by the half's writer lane
+__device__ __forceinline__ void tile_valid_store(const SearchArgs& a, int row, int c0_tile,
+                                                 bool valid, bool writer) {
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(valid);
+    const uint32_t half = (threadIdx.x & 32) ? (uint32_t)(bal >> 32) : (uint32_t)bal;
+    if (writer && c0_tile < a.cols)
+        a.row_valid[(size_t)row * a.valid_pitch + (c0_tile >> 5)] = (uint8_t)__popc(half);
+}
+
 // LIST block order: a wave's blocks start REV_AHEAD columns above its highest entry, a
 // workgroup's chunks at the chunk of its highest entry (REV_AHEAD_CHUNK = 0). Starting the
 // chunks 64 columns up as well sent every wave through the chunk above first, where only the
@@ -434,9 +462,16 @@ __device__ __forceinline__ void fused_agree(const AgreeArgs& g, int row, int c0,
 constexpr int FUSED_AGREE_N = 33;    // search_mx_kernel AG: 128-bit descriptors (cfg2, cfg5)
 constexpr int FUSED_AGREE_N_PK = 8;  // search_pk_kernel AG: 32-bit descriptors (cfg1)
 constexpr int REV_AHEAD_CHUNK = BICOS_REV_AHEAD_CHUNK;
+// kernel arguments: SearchArgs, plus the agree's for the fused (AG) instantiations only
+template <bool AG> struct SearchKArgs { using type = SearchArgs; };
+template <> struct SearchKArgs<true> { using type = SearchAgreeArgs; };
+__device__ __forceinline__ const SearchArgs& search_part(const SearchArgs& k) { return k; }
+__device__ __forceinline__ const SearchArgs& search_part(const SearchAgreeArgs& k) { return k.s; }
+
 template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIST, bool AG = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KSU >= 4 ? 3 : 4)))
-void search_mx_kernel(SearchArgs a) {
+void search_mx_kernel(typename SearchKArgs<AG>::type ka) {
+    const SearchArgs& a = search_part(ka);
     constexpr bool FK = KEYS == 3;
     static_assert(!FK || !NODUPES, "FK keys: first minimum only");
     constexpr bool XK = KEYS == 1 || KEYS == 2;
@@ -480,18 +515,22 @@ void search_mx_kernel(SearchArgs a) {
     int lcols = cols;
     const int e0 = c0_base + tile * waves * T * 32;
     int16_t* ent = nullptr;
+    // LIST, dense row (row_valid): identity entries, no prologue
+    bool dense = false;
     if constexpr (LIST) {
         constexpr int WLL = 2 * KSU;
         ent = (int16_t*)((char*)lds_mx + list_ent_offset(WLL * chunk * 16));
-        lcols = list_prologue(a.keep + (size_t)row * a.keep_pitch, cols, (uint32_t*)lds_mx, ent,
-                              e0, waves * T * 32);
+        dense = a.row_valid != nullptr && dense_row(a, row);
+        if (!dense)
+            lcols = list_prologue(a.keep + (size_t)row * a.keep_pitch, cols, (uint32_t*)lds_mx, ent,
+                                  e0, waves * T * 32);
         if (!TAIL) lcols = min(lcols, a.tail_col0);  // the tail launch takes the entries past it
         if (e0 >= lcols) return;  // the whole workgroup, past the prologue's barriers
     }
     // LIST: the column of entry i (ascending in i); the block order's start for entries < e
-    auto lcol = [&](int i) { return LIST ? (int)ent[i - e0] : i; };
+    auto lcol = [&](int i) { return LIST && !dense ? (int)ent[i - e0] : i; };
     auto start_col = [&](int e, int ahead) {
-        return LIST ? min(cols - 1, (int)ent[min(e, lcols) - 1 - e0] + ahead) : min(cols - 1, e - 1);
+        return LIST ? min(cols - 1, lcol(min(e, lcols) - 1) + ahead) : min(cols - 1, e - 1);
     };
 
     const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
@@ -895,6 +934,11 @@ void search_mx_kernel(SearchArgs a) {
     for (int t = 0; t < T; ++t) {
         if ((t & 1) != h) continue;  // half 0 writes even tiles, half 1 odd tiles
         const int c0i = c0_wave + 32 * t + jo;
+        if constexpr (!LIST && !AG) {  // dense-row fast path: this tile's valid count
+            if (a.row_valid)
+                tile_valid_store(a, row, c0_wave + 32 * t,
+                                 c0i < lcols && unique_of(t, best_of(t)), jo == 0);
+        }
         if (idle || c0i >= lcols) continue;
         const int c0 = lcol(c0i);
         const int best = best_of(t);
@@ -904,12 +948,15 @@ void search_mx_kernel(SearchArgs a) {
             v = ok ? (int16_t)(c0 - best) : INVALID_I16;
         else
             v = ok ? (int16_t)best : (int16_t)-1;
-        out[c0] = v;
-        if constexpr (AG) raw_lds[c0 - wg_c0] = v;
+        // (AG: only the agree reads the integer map, from LDS -- no HBM copy)
+        if constexpr (AG)
+            raw_lds[c0 - wg_c0] = v;
+        else
+            out[c0] = v;
     }
     if constexpr (AG) {
         __syncthreads();
-        fused_agree<FUSED_AGREE_N>(a.ag, row, wg_c0, min(waves * T * 32, cols - wg_c0), raw_lds);
+        fused_agree<FUSED_AGREE_N>(ka.ag, row, wg_c0, min(waves * T * 32, cols - wg_c0), raw_lds);
     }
 }
 
@@ -949,6 +996,17 @@ constexpr uint32_t LUT_PA = 0xAAA22A22u;  // right: bit 0 -> +1.0 (0x2), 1 -> -1
 constexpr uint32_t LUT_PB = 0x11199199u;  // left: bit 0 -> -0.5 (0x9), 1 -> +0.5 (0x1)
 constexpr int PK_SCALE_HI = 127 + 16;     // E8M0 2^16 for the K-half-0 (col0 P) lanes
 constexpr uint32_t PK_PAD = 0x7BFF7BFFu;
+// Lazy drops (round 6). A strict drop of the running minimum used to branch into (distance,
+// row) key trees that found its first row and whether the block holds it twice -- one
+// wave-uniform branch whenever any of the wave's 128 col0 dropped, ~150 VALU; on random
+// descriptors most blocks of a scan take it. Now a drop only records the block base (C) and
+// clears the tie marker, and each col0 rescans its final block once after the scan, from the
+// right row's raw words staged in LDS: 32 popcounts of WORDS words, the first col1 at the
+// minimum and whether it occurs twice (pk_rescan). BICOS_PK_LAZY=0 builds the branch (A/B).
+#ifndef BICOS_PK_LAZY
+#define BICOS_PK_LAZY 1
+#endif
+constexpr bool PK_LAZY = BICOS_PK_LAZY != 0;
 constexpr int PK_MAX_BITS = 127;
 constexpr int PK_MAX_COLS = 32767;
 
@@ -1017,7 +1075,8 @@ __device__ __forceinline__ v16f mfma_pk(v4i a, v4i b, v16f c, int sb) {
 // LIST: compacted col0 entries (as search_mx_kernel's)
 template <int WORDS, int T, bool TAIL, bool LIST, bool AG = false>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
-void search_pk_kernel(SearchArgs a) {
+void search_pk_kernel(typename SearchKArgs<AG>::type ka) {
+    const SearchArgs& a = search_part(ka);
     static_assert(T == 1 || T % 2 == 0, "wide tiles: 1 or pairs");
     static_assert(!AG || (!TAIL && !LIST), "the fused agree: main launch, every col0");
     constexpr int NP = T == 1 ? 1 : T / 2;
@@ -1047,16 +1106,19 @@ void search_pk_kernel(SearchArgs a) {
     int lcols = cols;
     const int e0 = c0_base + tile * waves * T * 64;
     int16_t* ent = nullptr;
+    bool dense = false;  // (as search_mx_kernel's)
     if constexpr (LIST) {
         ent = (int16_t*)((char*)lds_mx + list_ent_offset(WORDS * chunk * 16));
-        lcols = list_prologue(a.keep + (size_t)row * a.keep_pitch, cols, (uint32_t*)lds_mx, ent,
-                              e0, waves * T * 64);
+        dense = a.row_valid != nullptr && dense_row(a, row);
+        if (!dense)
+            lcols = list_prologue(a.keep + (size_t)row * a.keep_pitch, cols, (uint32_t*)lds_mx, ent,
+                                  e0, waves * T * 64);
         if (!TAIL) lcols = min(lcols, a.tail_col0);  // the tail launch takes the entries past it
         if (e0 >= lcols) return;  // the whole workgroup, past the prologue's barriers
     }
-    auto lcol = [&](int i) { return LIST ? (int)ent[i - e0] : i; };
+    auto lcol = [&](int i) { return LIST && !dense ? (int)ent[i - e0] : i; };
     auto start_col = [&](int e, int ahead) {
-        return LIST ? min(cols - 1, (int)ent[min(e, lcols) - 1 - e0] + ahead) : min(cols - 1, e - 1);
+        return LIST ? min(cols - 1, lcol(min(e, lcols) - 1) + ahead) : min(cols - 1, e - 1);
     };
 
     const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
@@ -1103,6 +1165,15 @@ void search_pk_kernel(SearchArgs a) {
         const auto sw = __builtin_amdgcn_permlane32_swap(x, y, false, false);
         const uint32_t comb = pkminu(sw[0], sw[1]);
         const uint32_t diff = pksub(comb, R[p]);
+        if constexpr (PK_LAZY) {
+            // a strict drop only records the block (branch-free); its first row and whether
+            // it holds the minimum twice are found once, after the scan (pk_rescan)
+            const uint32_t mi = pksign(diff);
+            M[p] = pkminu(M[p], diff) | mi;  // a drop: no tie seen since
+            R[p] = bfi(mi, comb, R[p]);
+            C[p] = bfi(mi, (uint32_t)B * 0x10001u, C[p]);
+            return;
+        }
         M[p] = pkminu(M[p], diff);
 #if defined(BICOS_PK_DIAG) && BICOS_PK_DIAG == 1  // timing only: the branch never runs
         const bool imp = (diff & 0x80008000u) == 0x80008001u;
@@ -1205,12 +1276,48 @@ void search_pk_kernel(SearchArgs a) {
             block(b, false);
         }
     }
-    if (!AG && idle) return;
     // AG: the workgroup's integer results go through LDS to the fused agree (as in
-    // search_mx_kernel); the chunk region is reused once every wave is done with its blocks
+    // search_mx_kernel); the chunk region is reused once every wave is done with its blocks.
+    // PK_LAZY: the right row's raw words are staged past those results when they fit (one
+    // coalesced copy per workgroup, L2-resident), for the rescans below; else read from HBM.
     int16_t* raw_lds = reinterpret_cast<int16_t*>(lds_mx);
     const int wg_c0 = c0_base + tile * waves * T * 64;
-    if constexpr (AG) __syncthreads();
+    const int row_off = (waves * T * 64 * 2 + 15) & ~15;  // bytes: past raw_lds
+    const bool staged = PK_LAZY && (size_t)WORDS * chunk * 16 >= (size_t)row_off + (size_t)cols * WORDS * 4;
+    if (!AG && !staged && idle) return;
+    if (AG || staged) __syncthreads();
+    uint32_t* row_lds = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds_mx) + row_off);
+    if (staged) {
+        const int nw = cols * WORDS;
+        if ((reinterpret_cast<uintptr_t>(row1) & 15u) == 0) {
+            for (int i = threadIdx.x; i < nw / 4; i += blockDim.x)
+                reinterpret_cast<v4i*>(row_lds)[i] = reinterpret_cast<const v4i*>(row1)[i];
+            for (int i = nw / 4 * 4 + threadIdx.x; i < nw; i += blockDim.x) row_lds[i] = row1[i];
+        } else {
+            for (int i = threadIdx.x; i < nw; i += blockDim.x) row_lds[i] = row1[i];
+        }
+        __syncthreads();
+        if (!AG && idle) return;
+    }
+    // PK_LAZY: col0 c's final block (base Bb, minimum distance hm) rescanned by popcounts --
+    // the first col1 at hm, and whether it occurs twice there; src = the right row's words
+    auto rescan = [&](const uint32_t* src, int c, int Bb, uint32_t hm, int& best, bool& uniq) {
+        uint32_t aw[WORDS];
+#pragma unroll
+        for (int w = 0; w < WORDS; ++w) aw[w] = row0[(size_t)c * WORDS + w];
+        uint32_t eq = 0;
+#pragma unroll 4
+        for (int r = 0; r < 32; ++r) {
+            const int c1 = Bb + r;
+            const int cc = min(c1, cols - 1);  // (past the row: never counted, read in bounds)
+            uint32_t hsum = 0;
+#pragma unroll
+            for (int w = 0; w < WORDS; ++w) hsum = __popc(aw[w] ^ src[(size_t)cc * WORDS + w]) + hsum;
+            eq |= (c1 < cols && hsum == hm) ? (1u << r) : 0u;
+        }
+        best = Bb + (int)__builtin_ctz(eq | 0x80000000u);
+        uniq = __popc(eq) == 1;
+    };
 
     int16_t* out = a.out + (size_t)row * a.out_pitch;
     int jo = j;
@@ -1222,28 +1329,55 @@ void search_pk_kernel(SearchArgs a) {
 #pragma unroll
         for (int f = 0; f < 2; ++f) {  // f = 0: high field (col0 P), 1: low field (Q = P + 32)
             const int c0i = c0_wave + 64 * t + 32 * f + jo;
-            if (idle || c0i >= lcols) continue;
-            const int c0 = lcol(c0i);
             const int sh = f ? 0 : 16;
-            const int best = (int)((C[p] >> sh) & 0xFFFFu);
-            const bool ok = ((M[p] >> sh) & 0xFFFFu) != 0u;
+            const bool live = !idle && c0i < lcols;
+            int best = (int)((C[p] >> sh) & 0xFFFFu);
+            bool ok = ((M[p] >> sh) & 0xFFFFu) != 0u;
+            if constexpr (PK_LAZY) {
+                // no tie in another block since the drop: count the final block's minima
+                if (live && ok) {
+                    const uint32_t hm = ((R[p] >> sh) & 0xFFFFu) - 0x4B00u;
+                    if (staged)
+                        rescan(row_lds, lcol(c0i), best, hm, best, ok);
+                    else
+                        rescan(row1, lcol(c0i), best, hm, best, ok);
+                }
+            }
+            if constexpr (!LIST && !AG) {  // dense-row fast path: this tile's valid count
+                if (a.row_valid)
+                    tile_valid_store(a, row, c0_wave + 64 * t + 32 * f, live && ok, jo == 0);
+            }
+            if (!live) continue;
+            const int c0 = lcol(c0i);
             int16_t v;
             if (a.out_mode == 0)
                 v = ok ? (int16_t)(c0 - best) : INVALID_I16;
             else
                 v = ok ? (int16_t)best : (int16_t)-1;
-            out[c0] = v;
-            if constexpr (AG) raw_lds[c0 - wg_c0] = v;
+            if constexpr (AG)
+                raw_lds[c0 - wg_c0] = v;
+            else
+                out[c0] = v;
         }
     }
     if constexpr (AG) {
         __syncthreads();
-        fused_agree<FUSED_AGREE_N_PK>(a.ag, row, wg_c0, min(waves * T * 64, cols - wg_c0), raw_lds);
+        fused_agree<FUSED_AGREE_N_PK>(ka.ag, row, wg_c0, min(waves * T * 64, cols - wg_c0), raw_lds);
     }
 }
 
+// kernel arguments of a launch: the search's, plus the agree's for AG
+template <bool AG>
+typename SearchKArgs<AG>::type kernel_args(const SearchArgs& a, const AgreeArgs* ag) {
+    if constexpr (AG)
+        return SearchAgreeArgs{a, *ag};
+    else
+        return a;
+}
+
 template <int WORDS, int T, bool TAIL, bool LIST = false, bool AG = false>
-hipError_t launch_pk_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st) {
+hipError_t launch_pk_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st,
+                          const AgreeArgs* ag = nullptr) {
     size_t lds = (size_t)WORDS * a.chunk * 16;
     if (LIST) lds = list_ent_offset((int)lds) + (size_t)waves * T * 64 * 2;
     const auto kern = search_pk_kernel<WORDS, T, TAIL, LIST, AG>;
@@ -1252,7 +1386,7 @@ hipError_t launch_pk_grid(const SearchArgs& a, int waves, int nwg, hipStream_t s
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * waves), lds, st, a);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * waves), lds, st, kernel_args<AG>(a, ag));
     return hipGetLastError();
 }
 
@@ -1306,7 +1440,8 @@ hipError_t launch_pk_w(const SearchArgs& a, const MxGeometry& g, hipStream_t st)
 }
 
 template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIST = false, bool AG = false>
-hipError_t launch_mx_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st) {
+hipError_t launch_mx_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st,
+                          const AgreeArgs* ag = nullptr) {
     constexpr int WL = 2 * KSU;
     size_t lds = (size_t)WL * a.chunk * 16;
     if (LIST) lds = list_ent_offset((int)lds) + (size_t)waves * T * 32 * 2;
@@ -1316,7 +1451,7 @@ hipError_t launch_mx_grid(const SearchArgs& a, int waves, int nwg, hipStream_t s
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * waves), lds, st, a);
+    hipLaunchKernelGGL(kern, dim3(nwg), dim3(64 * waves), lds, st, kernel_args<AG>(a, ag));
     return hipGetLastError();
 }
 
@@ -1513,7 +1648,8 @@ bool search_mx_agree_fusable(const MxGeometry& g, int words, bool nodupes, int c
            g.chunk * 4 * 16 >= 2 * 32 * g.T * g.waves;  // raw in LDS
 }
 
-hipError_t launch_search_mx_agree(SearchArgs a, const MxGeometry& g, hipStream_t st) {
+hipError_t launch_search_mx_agree(SearchArgs a, const AgreeArgs& ag, const MxGeometry& g,
+                                  hipStream_t st) {
     if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
     if (g.pk) {
         if (a.keep || a.out_mode != 0 || a.cols > PK_MAX_COLS || g.pk_chunk < 32 ||
@@ -1523,7 +1659,7 @@ hipError_t launch_search_mx_agree(SearchArgs a, const MxGeometry& g, hipStream_t
         a.tiles_per_row = g.pk_tiles_per_row;
         a.tail_T = 0;
         a.tail_col0 = a.cols;
-        return launch_pk_grid<1, 1, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st);
+        return launch_pk_grid<1, 1, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st, &ag);
     }
     if (a.keep || a.out_mode != 0 || a.cols > 32767 || g.chunk < 32 || (g.chunk & 31) ||
         g.waves < 1 || g.waves > 8 || (g.T != 4 && g.T != 2) || g.tail_T != 0)
@@ -1535,8 +1671,8 @@ hipError_t launch_search_mx_agree(SearchArgs a, const MxGeometry& g, hipStream_t
     a.tail_col0 = a.cols;
     // 2 tiles per wave: narrow row bands (N = 8 bands of cfg2, 192 rows)
     if (g.T == 2)
-        return launch_mx_grid<4, 2, true, 2, 2, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st);
-    return launch_mx_grid<4, 2, true, 4, 2, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st);
+        return launch_mx_grid<4, 2, true, 2, 2, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st, &ag);
+    return launch_mx_grid<4, 2, true, 4, 2, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st, &ag);
 }
 
 hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool nodupes,

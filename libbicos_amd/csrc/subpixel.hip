@@ -45,6 +45,7 @@ hipError_t launch_subpixel_t(const AgreeArgs& a, int depth, bool dbl, hipStream_
 hipError_t launch_subpixel(const AgreeArgs& a, int depth, bool dbl, hipStream_t st) {
     if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
     if (a.nsteps < 1) return hipErrorInvalidValue;
+    if (a.fwd) return hipErrorInvalidValue;  // (the Consistency check runs in the agree only)
     if (depth == 1)
         return dbl ? launch_subpixel_t<uint8_t, double>(a, depth, dbl, st)
                    : launch_subpixel_t<uint8_t, float>(a, depth, dbl, st);

@@ -165,6 +165,58 @@ class Engine:
         _lib.check(rc, "bicos_match_device")
         return out, corrmap
 
+    def plan(self, stack0: torch.Tensor, stack1: torch.Tensor,
+             cfg: Optional[MatchConfig] = None) -> int:
+        """bicos_match_plan: the _lib.PLAN_* bits of what match() runs past the transform for
+        these stacks and this config (fused launches, packed keys, compacted reverse search)."""
+        cfg = cfg or MatchConfig()
+        n, rows, cols, rp, pp = _check_stack(stack0)
+        c, has_nxcorr = cfg.to_c()
+        rc = self._L.bicos_match_plan(self._h, stack0.data_ptr(), stack1.data_ptr(), n, rows, cols,
+                                      rp, pp, _depth(stack0), ctypes.byref(c), has_nxcorr)
+        if rc < 0:
+            _lib.check(rc, "bicos_match_plan")
+        return rc
+
+    def search_agree(self, desc0: torch.Tensor, desc1: torch.Tensor, stack0: torch.Tensor,
+                     stack1: torch.Tensor, cfg: Optional[MatchConfig] = None,
+                     out: Optional[torch.Tensor] = None, corrmap: Optional[torch.Tensor] = None,
+                     stream=None) -> Tuple[torch.Tensor, Optional[torch.Tensor]]:
+        """bicos_search_agree_device: match() from its search on, over descriptors from
+        transform() of the two stacks -- the very launches match() issues after its
+        transform (bench.py times them in the frame)."""
+        cfg = cfg or MatchConfig()
+        n, rows, cols, rp, pp = _check_stack(stack0)
+        if tuple(stack1.shape) != (n, rows, cols) or stack1.stride() != stack0.stride() or \
+                stack1.dtype != stack0.dtype:
+            raise ValueError("stack1 must match stack0 in shape, strides and dtype")
+        words = descriptor_words(n, cfg.mode)
+        pitch = self._L.bicos_desc_pitch(cols, words)
+        for name, d in (("desc0", desc0), ("desc1", desc1)):
+            if d.device != stack0.device or d.dtype != torch.int32 or not d.is_contiguous() or \
+                    tuple(d.shape) != (rows, pitch):
+                raise ValueError("%s must be a contiguous int32 [%d, %d] tensor on %s"
+                                 % (name, rows, pitch, stack0.device))
+        c, has_nxcorr = cfg.to_c()
+        dev = stack0.device
+        disp_dtype = torch.float32 if has_nxcorr else torch.int16
+        corr_dtype = torch.float64 if cfg.precision else torch.float32
+        if out is None:
+            out = torch.empty((rows, cols), dtype=disp_dtype, device=dev)
+        _check_out(out, "out", (rows, cols), (disp_dtype,), dev)
+        if has_nxcorr and corrmap is None:
+            corrmap = torch.empty((rows, cols), device=dev, dtype=corr_dtype)
+        if not has_nxcorr:
+            corrmap = None
+        if corrmap is not None:
+            _check_out(corrmap, "corrmap", (rows, cols), (corr_dtype,), dev)
+        rc = self._L.bicos_search_agree_device(
+            self._h, desc0.data_ptr(), desc1.data_ptr(), stack0.data_ptr(), stack1.data_ptr(),
+            n, rows, cols, rp, pp, _depth(stack0), ctypes.byref(c), has_nxcorr, out.data_ptr(),
+            corrmap.data_ptr() if corrmap is not None else None, _stream(dev, stream))
+        _lib.check(rc, "bicos_search_agree_device")
+        return out, corrmap
+
     # ----------------------------------------------------------------- stages
     def transform(self, stack: torch.Tensor, mode: int = 0, words: Optional[int] = None,
                   out: Optional[torch.Tensor] = None, stream=None) -> torch.Tensor:

@@ -9,6 +9,7 @@ import contextlib
 import numpy as np
 import pytest
 
+from libbicos_amd import _lib
 from libbicos_amd.synthetic import random_stack, stereo_stack
 from oracle import ref_numpy as N
 
@@ -1222,6 +1223,8 @@ def test_fused_search_agree_equals_stages(gpu, H, W, kw):
     L[:, 5, 200:260] = 9  # flat patch: NaN / low-variance correlations
     s0, s1 = dev(L), dev(R)
     cfg = MatchConfig(**kw)
+    #  the match of this shape really runs the fused launch
+    assert gpu.plan(s0, s1, cfg) & _lib.PLAN_AGREE_IN_SEARCH
     md, mc = gpu.match(s0, s1, cfg)
     words = descriptor_words(n, 0)
     raw = gpu.search(gpu.transform(s0, 0, words), gpu.transform(s1, 0, words), W, words, 1)
@@ -1247,6 +1250,8 @@ def test_fused_pk_search_agree_equals_stages(gpu, H, W):
     L[:, 3, 100:150] = 11  # flat patch
     s0, s1 = dev(L), dev(R)
     cfg = MatchConfig(nxcorr_threshold=0.9)
+    plan = gpu.plan(s0, s1, cfg)
+    assert plan & _lib.PLAN_AGREE_IN_SEARCH and plan & _lib.PLAN_PACKED_KEYS
     md, mc = gpu.match(s0, s1, cfg)
     words = descriptor_words(n, 0)
     d0, d1 = gpu.transform(s0, 0, words), gpu.transform(s1, 0, words)
@@ -1258,3 +1263,128 @@ def test_fused_pk_search_agree_equals_stages(gpu, H, W):
     io, ic = gpu.match(s0, s1, cfg, out=io)
     same(host(io).astype(np.float32), host(md))
     same(host(ic), host(mc))
+
+
+# ------------------------ the row bands an N-GPU run matches, against the oracle
+# bench.py --gpus N splits cfg2's 1536 rows into N bands of 1536 / N; each rank matches its
+# band alone, so the band's grid is what the N-GPU run executes (192 rows at N = 8: the
+# 2-tile fused search + agree). Each band, matched as its own frame, must
+# equal the oracle's whole-frame fixture on those rows: frames.json holds the C oracle's
+# sha256 of every 64-row band of cfg2 (tests/golden/make_frames.py), disparity and corrmap.
+# Reference semantics: agree.hpp:53-93, bicos.hpp:78-113 (row-local, so a band is exact).
+@pytest.mark.parametrize("N", [8, 4, 2])
+def test_cfg2_row_bands_match_oracle_fixture(gpu, N):
+    from libbicos_amd.device import MatchConfig
+    from libbicos_amd.distributed import band_rows
+    from tests.golden.make_frames import band_hashes, sha
+    rec = _frames()["cfg2"]
+    n, H, W, B = rec["n"], rec["H"], rec["W"], rec["band_rows"]
+    L, R = _frame_stacks(n, H, W)
+    assert [sha(L), sha(R)] == rec["inputs_sha256"], "synthetic generator changed"
+    s0, s1 = dev(L), dev(R)
+    cfg = MatchConfig(**rec["config"])
+    for r in range(N):
+        b, e = band_rows(H, N, r)
+        assert (e - b) % B == 0 and b % B == 0
+        t0, t1 = s0[:, b:e], s1[:, b:e]
+        # the band shape takes the fused search + agree launch (2 tiles per wave at N = 8)
+        assert gpu.plan(t0, t1, cfg) & _lib.PLAN_AGREE_IN_SEARCH, (N, r)
+        d, c = gpu.match(t0, t1, cfg)
+        hd, hc = host(d), host(c)
+        assert band_hashes(hd, B) == rec["disparity_bands"][b // B:e // B], ("disparity", N, r)
+        assert band_hashes(hc, B) == rec["corrmap_bands"][b // B:e // B], ("corrmap", N, r)
+
+
+# ---------------------------- the match past its transform (bicos_search_agree_device)
+# bench.py times the launches the match issues after its transform through this entry; it
+# must produce the match's maps for every plan: fused search + agree (cfg1 / cfg2 shapes),
+# search + subpixel (cfg3), Consistency with its check inside the agree (cfg4), no NXC.
+@pytest.mark.parametrize("n,H,W,dt,kw", [
+    (8, 64, 640, np.uint8, dict(nxcorr_threshold=0.9)),
+    (33, 300, 2048, np.uint8, dict(nxcorr_threshold=0.96)),
+    (33, 40, 1024, np.uint8, dict(nxcorr_threshold=0.96, min_variance=2.0, subpixel_step=0.1)),
+    (40, 24, 1100, np.uint8, dict(nxcorr_threshold=0.96, variant=1, max_lr_diff=1)),
+    (17, 9, 700, np.uint16, dict(nxcorr_threshold=0.8, variant=1, max_lr_diff=0, no_dupes=True)),
+    (12, 16, 500, np.uint8, dict(nxcorr_threshold=None)),
+])
+def test_search_agree_entry_equals_match(gpu, n, H, W, dt, kw):
+    from libbicos_amd.device import MatchConfig, descriptor_words
+    L, R = stereo_stack(n, H, W, dt, dmin=3, drange=40, seed=n + W)
+    s0, s1 = dev(L), dev(R)
+    cfg = MatchConfig(**kw)
+    md, mc = gpu.match(s0, s1, cfg)
+    words = descriptor_words(n, 0)
+    d0, d1 = gpu.transform(s0, 0, words), gpu.transform(s1, 0, words)
+    sd, sc = gpu.search_agree(d0, d1, s0, s1, cfg)
+    same(host(sd), host(md))
+    if mc is not None:
+        same(host(sc), host(mc))
+
+
+# -------------------- Consistency's left-right check inside the agree (agree_lds_kernel CONS)
+# With NXC and aligned stacks the check of consistency_kernel (bicos.hpp:99-106) runs in the
+# agree launch (bicos_match_plan PLAN_CONSISTENCY_IN_AGREE): every max_lr_diff, with and
+# without NoDuplicates, u8 / u16, min-variance, against the oracle; a subpixel config
+# keeps the separate check kernel.
+@pytest.mark.parametrize("n,H,W,dt,kw", [
+    (40, 6, 2048, np.uint8, dict(nxcorr_threshold=0.96, variant=1, max_lr_diff=1)),
+    (40, 5, 1300, np.uint8, dict(nxcorr_threshold=0.5, variant=1, max_lr_diff=0, no_dupes=True)),
+    (9, 7, 332, np.uint8, dict(nxcorr_threshold=0.7, variant=1, max_lr_diff=5, min_variance=1.0)),
+    (17, 6, 900, np.uint16, dict(nxcorr_threshold=0.8, variant=1, max_lr_diff=2)),
+    (33, 4, 1032, np.uint8, dict(nxcorr_threshold=0.9, variant=1, max_lr_diff=3)),
+    (65, 3, 260, np.uint8, dict(nxcorr_threshold=0.2, variant=1, max_lr_diff=1)),
+])
+def test_consistency_in_agree(gpu, oracle, n, H, W, dt, kw):
+    from libbicos_amd.device import MatchConfig
+    L, R = stereo_stack(n, H, W, dt, dmin=2, drange=50, seed=n * 7 + W)
+    L[:, 1, 40:90] = 5  # flat patch: NaN correlations pass
+    s0, s1 = dev(L), dev(R)
+    cfg = MatchConfig(**kw)
+    assert gpu.plan(s0, s1, cfg) & _lib.PLAN_CONSISTENCY_IN_AGREE
+    d, c = gpu.match(s0, s1, cfg)
+    rd, rc = oracle.match(L, R, oracle.OracleConfig(**kw))
+    same(host(d), rd)
+    same(host(c), rc)
+    # both precisions against the two-launch form: the check alone (no NXC: the int16 map of
+    # consistency_kernel), then the agree stage on it
+    raw, _ = gpu.match(s0, s1, MatchConfig(**dict(kw, nxcorr_threshold=None)))
+    mv = kw.get("min_variance")
+    mv = None if mv is None else float(np.float32(mv) * np.float32(n))
+    for prec in (0, 1):
+        pd, pc = gpu.match(s0, s1, MatchConfig(**dict(kw, precision=prec)))
+        ad, ac = gpu.agree(raw, s0, s1, kw["nxcorr_threshold"], mv, precision=prec)
+        same(host(pd), host(ad))
+        same(host(pc), host(ac))
+    sub = MatchConfig(**dict(kw, subpixel_step=0.25))
+    assert not gpu.plan(s0, s1, sub) & _lib.PLAN_CONSISTENCY_IN_AGREE
+
+
+# ------------------------ Consistency's dense-row fast path (search_mx.hip dense_row)
+# Rows whose forward search kept >= 7/8 of their col0 run the reverse search over every col0
+# instead of the compacted entries; sparse rows keep the prologue. A frame mixing both (planted
+# stereo rows, rows with an unrelated right image, rows between) against the oracle, every
+# width class of the search (packed keys, one-product keys 128 / 256-bit, FK keys).
+@pytest.mark.parametrize("n,W,kw", [
+    (40, 700, dict(variant=1, max_lr_diff=1)),
+    (40, 2048, dict(variant=1, max_lr_diff=2, no_dupes=True)),
+    (33, 1100, dict(variant=1, max_lr_diff=1)),
+    (8, 900, dict(variant=1, max_lr_diff=0, no_dupes=True)),
+    (17, 640, dict(variant=1, max_lr_diff=3)),
+])
+@pytest.mark.parametrize("nxc", [None, 0.8])
+def test_consistency_dense_rows(gpu, oracle, n, W, kw, nxc):
+    from libbicos_amd.device import MatchConfig
+    H = 12
+    L, R = stereo_stack(n, H, W, dmin=2, drange=40, seed=n + W)
+    Rr = random_stack(n, H, W, seed=n * W)
+    R[:, 4:8] = Rr[:, 4:8]            # rows 4-7: nothing to match -> sparse rows
+    R[:, 8:10, W // 2:] = Rr[:, 8:10, W // 2:]  # rows 8-9: half of each row matches
+    cfg = dict(kw, nxcorr_threshold=nxc)
+    s0, s1 = dev(L), dev(R)
+    plan = gpu.plan(s0, s1, MatchConfig(**cfg))
+    assert plan & _lib.PLAN_DENSE_ROWS and plan & _lib.PLAN_REVERSE_COMPACTED
+    d, c = gpu.match(s0, s1, MatchConfig(**cfg))
+    rd, rc = oracle.match(L, R, oracle.OracleConfig(**cfg))
+    same(host(d), rd)
+    if rc is not None:
+        same(host(c), rc)
