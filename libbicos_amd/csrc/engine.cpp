@@ -528,14 +528,36 @@ int match_host(bicos_engine* e, const void* const* p0, const size_t* steps0,
         e->pool.reset(new HostPool((int)std::max(1u, std::min(cap, hw ? hw : 1u))));
     }
 
-    // The maps: band by band on dl_stream into pinned memory as each band's match ends,
-    // overlapping the later bands' uploads (round 6, VERDICT r05 #8: the round-5 band-wise
-    // download shared the upload stream's copy engine), then into the caller's buffers by the
-    // pool. BICOS_HOST_DL=once: one download of each map at the end (round 5).
+    // Round 6 (profiles/host_path_r06.jsonl, host_trace_r06*.txt): each band's
+    // upload is split over two copy streams, and the maps come down band by band on a third
+    // stream into pinned memory as each band's match ends, then into the caller's buffers by
+    // the pool -- 4.40-4.52 ms per cfg2 match against 5.45-5.79 with one upload stream and one
+    // download at the end (two rounds interleaved on one box; either change alone was not
+    // consistent: 4.86-7.29 / 4.98-5.41 ms). BICOS_HOST_UPLOAD_STREAMS=1 / BICOS_HOST_DL=once:
+    // the round-5 pipeline.
     static const bool dl_bands = [] {
         const char* v = std::getenv("BICOS_HOST_DL");
         return !(v && !std::strcmp(v, "once"));
     }();
+    static const int up_streams = [] {
+        const char* v = std::getenv("BICOS_HOST_UPLOAD_STREAMS");
+        return v && std::atoi(v) == 1 ? 1 : 2;
+    }();
+    if (up_streams == 2) {
+        if (!e->copy_stream2) {
+            rc = check_hip(hipStreamCreateWithFlags(&e->copy_stream2, hipStreamNonBlocking),
+                           "hipStreamCreate");
+            if (rc) return rc;
+        }
+        while ((int)e->events2.size() < B) {
+            hipEvent_t ev;
+            rc = check_hip(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+            if (rc) return rc;
+            e->events2.push_back(ev);
+        }
+        rc = check_hip(hipStreamWaitEvent(e->copy_stream2, e->ws_ready, 0), "hipStreamWaitEvent");
+        if (rc) return rc;
+    }
     const size_t corr_bytes = corr ? (size_t)rows * cols * csz : 0;
     if (dl_bands) {
         if (!e->dl_stream) {
@@ -586,6 +608,8 @@ int match_host(bicos_engine* e, const void* const* p0, const size_t* steps0,
         char* slot = (char*)e->pinned + (size_t)(b % K) * band_bytes;
         if (b >= K) {
             rc = check_hip(hipEventSynchronize(e->events[b - K]), "hipEventSynchronize");
+            if (!rc && up_streams == 2)
+                rc = check_hip(hipEventSynchronize(e->events2[b - K]), "hipEventSynchronize");
             if (rc) break;
         }
         char* band = dev + (size_t)b * band_bytes;
@@ -613,8 +637,15 @@ int match_host(bicos_engine* e, const void* const* p0, const size_t* steps0,
             (void)hipEventCreate(&t1);
             (void)hipEventRecord(t0, ks);
         }
-        rc = check_hip(hipMemcpyAsync(band, slot, 2 * (size_t)n * plane, hipMemcpyHostToDevice, ks),
-                       "stack upload");
+        const size_t up = 2 * (size_t)n * plane;
+        const size_t first = up_streams == 2 ? (up / 2 + 4095) / 4096 * 4096 : up;
+        rc = check_hip(hipMemcpyAsync(band, slot, first, hipMemcpyHostToDevice, ks), "stack upload");
+        if (!rc && first < up) {
+            rc = check_hip(hipMemcpyAsync(band + first, slot + first, up - first,
+                                          hipMemcpyHostToDevice, e->copy_stream2), "stack upload");
+            if (!rc) rc = check_hip(hipEventRecord(e->events2[b], e->copy_stream2), "hipEventRecord");
+            if (!rc) rc = check_hip(hipStreamWaitEvent(cs, e->events2[b], 0), "hipStreamWaitEvent");
+        }
         if (trace) {
             (void)hipEventRecord(t1, ks);
             dma_ev.push_back({t0, t1});
@@ -676,6 +707,7 @@ int match_host(bicos_engine* e, const void* const* p0, const size_t* steps0,
     }
     // drain every stream whatever happened: the slots and the stage are reused next call
     const int r1 = check_hip(hipStreamSynchronize(ks), "hipStreamSynchronize");
+    if (up_streams == 2) (void)hipStreamSynchronize(e->copy_stream2);
     const int r2 = check_hip(hipStreamSynchronize(cs), "hipStreamSynchronize");
     const int r3 = dl_bands ? check_hip(hipStreamSynchronize(e->dl_stream), "hipStreamSynchronize")
                             : BICOS_OK;
@@ -786,6 +818,8 @@ void bicos_engine_destroy(bicos_engine* e) {
     if (e->pinned_out) (void)hipHostFree(e->pinned_out);
     for (hipEvent_t ev : e->dl_events) (void)hipEventDestroy(ev);
     if (e->dl_stream) (void)hipStreamDestroy(e->dl_stream);
+    if (e->copy_stream2) (void)hipStreamDestroy(e->copy_stream2);
+    for (hipEvent_t ev : e->events2) (void)hipEventDestroy(ev);
     e->pool.reset();
     if (e->own_stream) (void)hipStreamDestroy(e->own_stream);
     if (e->copy_stream) (void)hipStreamDestroy(e->copy_stream);

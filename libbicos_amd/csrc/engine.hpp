@@ -75,6 +75,9 @@ struct bicos_engine {
     // engine other than the uploads' can take them: PCIe is full duplex) into pinned memory,
     // then copied into the caller's buffers by the pool; 2 events per band (matched, landed)
     hipStream_t dl_stream = nullptr;
+    // a second upload stream: each band's upload split in two halves (BICOS_HOST_UPLOAD_STREAMS)
+    hipStream_t copy_stream2 = nullptr;
+    std::vector<hipEvent_t> events2;
     void* pinned_out = nullptr;
     size_t pinned_out_bytes = 0;
     std::vector<hipEvent_t> dl_events;

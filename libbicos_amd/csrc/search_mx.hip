@@ -374,11 +374,16 @@ __device__ __forceinline__ bool dense_row(const SearchArgs& a, int row) {
     return __builtin_amdgcn_readfirstlane(sum) * 8 >= 7 * a.cols;
 }
 // forward search epilogue, dense-row fast path: the valid results of one 32-col0 tile (the
-// 32 lanes of this lane's half-wave, lane & 31 = col0 % 32) counted into
-// row_valid[row][c0_tile / 32] by the half's writer lane
+// 32 lanes of this lane's half-wave, lane & 31 = col0 % 32) whose col1 `best` lies above the
+// previous col0's (a rectified stereo row's matches ascend with col0, so the count stands for
+// the DISTINCT col1 the reverse search needs; random descriptors, whose every col0 may be
+// valid, count about half), counted into row_valid[row][c0_tile / 32] by the half's writer
 __device__ __forceinline__ void tile_valid_store(const SearchArgs& a, int row, int c0_tile,
-                                                 bool valid, bool writer) {
-    const uint64_t bal = __builtin_amdgcn_ballot_w64(valid);
+                                                 bool valid, int best, bool writer) {
+    const int v = valid ? best : -1;
+    const int prev = __shfl_up(v, 1, 32);  // (the half's first lane: its own value)
+    const bool first = (threadIdx.x & 31) == 0;
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(valid && (first || v > prev));
     const uint32_t half = (threadIdx.x & 32) ? (uint32_t)(bal >> 32) : (uint32_t)bal;
     if (writer && c0_tile < a.cols)
         a.row_valid[(size_t)row * a.valid_pitch + (c0_tile >> 5)] = (uint8_t)__popc(half);
@@ -937,7 +942,7 @@ void search_mx_kernel(typename SearchKArgs<AG>::type ka) {
         if constexpr (!LIST && !AG) {  // dense-row fast path: this tile's valid count
             if (a.row_valid)
                 tile_valid_store(a, row, c0_wave + 32 * t,
-                                 c0i < lcols && unique_of(t, best_of(t)), jo == 0);
+                                 c0i < lcols && unique_of(t, best_of(t)), best_of(t), jo == 0);
         }
         if (idle || c0i >= lcols) continue;
         const int c0 = lcol(c0i);
@@ -1073,12 +1078,13 @@ __device__ __forceinline__ v16f mfma_pk(v4i a, v4i b, v16f c, int sb) {
 // T wide tiles (64 col0 each) per wave; T = 1 or an even count (tiles reduced in pairs);
 // TAIL: the col0 range starts at a.tail_col0 (the tail launch, as search_mx_kernel's);
 // LIST: compacted col0 entries (as search_mx_kernel's)
-template <int WORDS, int T, bool TAIL, bool LIST, bool AG = false>
+template <int WORDS, int T, bool TAIL, bool LIST, bool AG = false, bool LAZY = PK_LAZY>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void search_pk_kernel(typename SearchKArgs<AG>::type ka) {
     const SearchArgs& a = search_part(ka);
     static_assert(T == 1 || T % 2 == 0, "wide tiles: 1 or pairs");
     static_assert(!AG || (!TAIL && !LIST), "the fused agree: main launch, every col0");
+    static_assert(!AG || WORDS == 1 || WORDS == 4, "the fused agree: cfg1's and cfg2's widths");
     constexpr int NP = T == 1 ? 1 : T / 2;
     extern __shared__ __attribute__((aligned(16))) v4i lds_mx[];  // [WORDS][chunk]
 
@@ -1165,13 +1171,17 @@ void search_pk_kernel(typename SearchKArgs<AG>::type ka) {
         const auto sw = __builtin_amdgcn_permlane32_swap(x, y, false, false);
         const uint32_t comb = pkminu(sw[0], sw[1]);
         const uint32_t diff = pksub(comb, R[p]);
-        if constexpr (PK_LAZY) {
+        if constexpr (LAZY) {
             // a strict drop only records the block (branch-free); its first row and whether
             // it holds the minimum twice are found once, after the scan (pk_rescan)
             const uint32_t mi = pksign(diff);
             M[p] = pkminu(M[p], diff) | mi;  // a drop: no tie seen since
             R[p] = bfi(mi, comb, R[p]);
-            C[p] = bfi(mi, (uint32_t)B * 0x10001u, C[p]);
+            // (one v_bfi_b32 with the block base as an SGPR operand: left alone, the compiler
+            // rebuilt the per-field select from two compares, two cndmasks and a v_perm)
+            uint32_t c = C[p];
+            asm("v_bfi_b32 %0, %1, %2, %0" : "+v"(c) : "v"(mi), "s"((uint32_t)B * 0x10001u));
+            C[p] = c;
             return;
         }
         M[p] = pkminu(M[p], diff);
@@ -1283,7 +1293,7 @@ void search_pk_kernel(typename SearchKArgs<AG>::type ka) {
     int16_t* raw_lds = reinterpret_cast<int16_t*>(lds_mx);
     const int wg_c0 = c0_base + tile * waves * T * 64;
     const int row_off = (waves * T * 64 * 2 + 15) & ~15;  // bytes: past raw_lds
-    const bool staged = PK_LAZY && (size_t)WORDS * chunk * 16 >= (size_t)row_off + (size_t)cols * WORDS * 4;
+    const bool staged = LAZY && (size_t)WORDS * chunk * 16 >= (size_t)row_off + (size_t)cols * WORDS * 4;
     if (!AG && !staged && idle) return;
     if (AG || staged) __syncthreads();
     uint32_t* row_lds = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds_mx) + row_off);
@@ -1333,7 +1343,7 @@ void search_pk_kernel(typename SearchKArgs<AG>::type ka) {
             const bool live = !idle && c0i < lcols;
             int best = (int)((C[p] >> sh) & 0xFFFFu);
             bool ok = ((M[p] >> sh) & 0xFFFFu) != 0u;
-            if constexpr (PK_LAZY) {
+            if constexpr (LAZY) {
                 // no tie in another block since the drop: count the final block's minima
                 if (live && ok) {
                     const uint32_t hm = ((R[p] >> sh) & 0xFFFFu) - 0x4B00u;
@@ -1345,7 +1355,7 @@ void search_pk_kernel(typename SearchKArgs<AG>::type ka) {
             }
             if constexpr (!LIST && !AG) {  // dense-row fast path: this tile's valid count
                 if (a.row_valid)
-                    tile_valid_store(a, row, c0_wave + 64 * t + 32 * f, live && ok, jo == 0);
+                    tile_valid_store(a, row, c0_wave + 64 * t + 32 * f, live && ok, best, jo == 0);
             }
             if (!live) continue;
             const int c0 = lcol(c0i);
@@ -1362,7 +1372,9 @@ void search_pk_kernel(typename SearchKArgs<AG>::type ka) {
     }
     if constexpr (AG) {
         __syncthreads();
-        fused_agree<FUSED_AGREE_N_PK>(ka.ag, row, wg_c0, min(waves * T * 64, cols - wg_c0), raw_lds);
+        // (n = 8 with 32-bit descriptors, cfg1; n = 33 with 128-bit, cfg2 / cfg5)
+        fused_agree<WORDS == 1 ? FUSED_AGREE_N_PK : FUSED_AGREE_N>(
+            ka.ag, row, wg_c0, min(waves * T * 64, cols - wg_c0), raw_lds);
     }
 }
 
@@ -1375,12 +1387,21 @@ typename SearchKArgs<AG>::type kernel_args(const SearchArgs& a, const AgreeArgs*
         return a;
 }
 
+// Lazy drops pay a fixed rescan per col0 (~32 popcounts of WORDS words); the drop branch
+// pays per drop. Narrow rows (few blocks, few drops on stereo input) keep the branch: cfg1
+// (640 columns) 13391 vs 12478-12791 Mpix/s; 3208-3300-column rows take the lazy form: random
+// 32-bit NoDuplicates 0.66 vs 1.12-1.14 ms, FULL n = 6 +5 % (FULL n = 8 -1.7 %);
+// profiles/pk_lazy_r06.jsonl
+constexpr int PK_LAZY_MIN_COLS = 1024;
+
 template <int WORDS, int T, bool TAIL, bool LIST = false, bool AG = false>
 hipError_t launch_pk_grid(const SearchArgs& a, int waves, int nwg, hipStream_t st,
                           const AgreeArgs* ag = nullptr) {
     size_t lds = (size_t)WORDS * a.chunk * 16;
     if (LIST) lds = list_ent_offset((int)lds) + (size_t)waves * T * 64 * 2;
-    const auto kern = search_pk_kernel<WORDS, T, TAIL, LIST, AG>;
+    const bool lazy = PK_LAZY && a.cols >= PK_LAZY_MIN_COLS;
+    const auto kern = lazy ? search_pk_kernel<WORDS, T, TAIL, LIST, AG, PK_LAZY>
+                           : search_pk_kernel<WORDS, T, TAIL, LIST, AG, false>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1607,12 +1628,20 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     }
     // packed keys: the default NoDuplicates search for 32/64-bit descriptors (one K-step,
     // where the key reduction, not the matrix products, bounds the one-product search: FULL
-    // n = 6 0.63 vs 1.43 ms, n = 8 0.78 vs 0.97 ms at 3208x2200, profiles/search_integ_r04.jsonl;
-    // at 128 bits it measured slower, 0.336 vs 0.311 ms at cfg2, profiles/pk_keys_r03.jsonl),
+    // n = 6 0.63 vs 1.43 ms, n = 8 0.78 vs 0.97 ms at 3208x2200, profiles/search_integ_r04.jsonl)
+    // and, since its drops became lazy (round 6), for 128-bit descriptors with <= 127 used
+    // bits too (LIMITED n <= 33, FULL n <= 12): cfg2 0.334 vs 0.349 ms, cfg5 1.364 vs 1.446,
+    // readme 1.073 vs 1.078, random cfg2 0.382 vs 0.481 (profiles/pk128_r06.jsonl; round 3,
+    // with the drop branch, it measured slower: 0.336 vs 0.311 ms, pk_keys_r03.jsonl);
     // or wherever variant 68 asks for it. Same workgroup shape, a wide tile = two 32-col0
     // tiles; the LDS stage holds one expanded word per descriptor word
     // (32/64-bit words need no used-bits hint: a distance is at most 64 <= PK_MAX_BITS)
-    g.pk = (keys == 4 || (keys == 0 && words <= 2)) &&
+    // (BICOS_PK128=0: the one-product search for 128-bit descriptors again; A/B, read once)
+    static const bool pk128 = [] {
+        const char* v = std::getenv("BICOS_PK128");
+        return !(v && !std::strcmp(v, "0"));
+    }();
+    g.pk = (keys == 4 || (keys == 0 && (words <= 2 || (words == 4 && PK_LAZY && pk128)))) &&
            (words <= 2 || (bits > 0 && bits <= PK_MAX_BITS)) && bits <= 32 * words &&
            (words == 1 || words == 2 || words == 4) && cols <= PK_MAX_COLS;
     g.pk_T = g.T >= 2 ? g.T / 2 : 1;
@@ -1637,11 +1666,14 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
 bool search_mx_agree_fusable(const MxGeometry& g, int words, bool nodupes, int cols, int n,
                              int depth, bool dbl) {
     if (!nodupes || depth != 1 || dbl) return false;
-    // packed keys, 32-bit words, one wide tile per wave, no tail; the raw results (64 int16
-    // per wave) in the LDS stage (16 B per col1)
+    // packed keys: 32-bit words with one wide tile per wave and n = 8 (cfg1), 128-bit words
+    // with one or two and n = 33 (cfg2, cfg5, their row bands); no tail; the raw results (64
+    // int16 per wave and wide tile) in the LDS stage (16 B per col1 and word)
     if (g.pk)
-        return words == 1 && g.pk_T == 1 && g.pk_tail_col0 == cols && n == FUSED_AGREE_N_PK &&
-               cols <= PK_MAX_COLS && g.pk_chunk * 16 >= 128 * g.waves;
+        return ((words == 1 && g.pk_T == 1 && n == FUSED_AGREE_N_PK) ||
+                (words == 4 && (g.pk_T == 1 || g.pk_T == 2) && n == FUSED_AGREE_N)) &&
+               g.pk_tail_col0 == cols && cols <= PK_MAX_COLS &&
+               (long)g.pk_chunk * words * 16 >= 128L * g.waves * g.pk_T;
     // launch_mx_t's key choice for this shape is KEYS 2 (NoDuplicates, cols <= XKF_MAX_COLS)
     return words == 4 && g.ksteps == 2 && g.keys == 1 && cols <= XKF_MAX_COLS &&
            (g.T == 4 || g.T == 2) && g.tail_T == 0 && n == FUSED_AGREE_N &&
@@ -1653,13 +1685,20 @@ hipError_t launch_search_mx_agree(SearchArgs a, const AgreeArgs& ag, const MxGeo
     if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
     if (g.pk) {
         if (a.keep || a.out_mode != 0 || a.cols > PK_MAX_COLS || g.pk_chunk < 32 ||
-            (g.pk_chunk & 31) || g.waves < 1 || g.waves > 8 || g.pk_T != 1 || g.pk_tail_col0 != a.cols)
+            (g.pk_chunk & 31) || g.waves < 1 || g.waves > 8 || g.pk_tail_col0 != a.cols)
             return hipErrorInvalidValue;
         a.chunk = g.pk_chunk;
         a.tiles_per_row = g.pk_tiles_per_row;
         a.tail_T = 0;
         a.tail_col0 = a.cols;
-        return launch_pk_grid<1, 1, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st, &ag);
+        const int nwg = a.rows * a.tiles_per_row;
+        if (ag.n == FUSED_AGREE_N_PK && g.pk_T == 1)
+            return launch_pk_grid<1, 1, false, false, true>(a, g.waves, nwg, st, &ag);
+        if (ag.n == FUSED_AGREE_N && g.pk_T == 1)
+            return launch_pk_grid<4, 1, false, false, true>(a, g.waves, nwg, st, &ag);
+        if (ag.n == FUSED_AGREE_N && g.pk_T == 2)
+            return launch_pk_grid<4, 2, false, false, true>(a, g.waves, nwg, st, &ag);
+        return hipErrorInvalidValue;
     }
     if (a.keep || a.out_mode != 0 || a.cols > 32767 || g.chunk < 32 || (g.chunk & 31) ||
         g.waves < 1 || g.waves > 8 || (g.T != 4 && g.T != 2) || g.tail_T != 0)

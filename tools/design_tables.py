@@ -1,6 +1,6 @@
 """Regenerate the measured tables of DESIGN.md §8 from the committed bench records:
-profiles/bench_r05.jsonl (the 6 BASELINE configs, then the 20 lines of the reference integration
-grid), with profiles/bench_r04.jsonl as the round-4 column. The tables sit between
+profiles/bench_r06.jsonl (the 6 BASELINE configs, then the 20 lines of the reference integration
+grid), with profiles/bench_r05.jsonl as the round-5 column. The tables sit between
 <!-- BENCH_TABLE --> / <!-- INTEG_TABLE --> markers.
 
   python tools/design_tables.py
@@ -12,15 +12,16 @@ import re
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 P = os.path.join(ROOT, "profiles")
 
-CUR, PREV = "bench_r05.jsonl", "bench_r04.jsonl"
-DRIVER_PREV = {"cfg2": " (driver 7865)"}
+CUR, PREV = "bench_r06.jsonl", "bench_r05.jsonl"
+DRIVER_PREV = {"cfg2": " (driver 7718)"}
 
 
 def bound_text(r):
-    if r["bound"] == "valu":
-        return "%.3f of its key-reduction issue bound (%.3f of dense FP4)" % (
-            r["frac"], r["fp4_view"]["frac"])
-    return "%.3f of dense FP4" % r["frac"]
+    bm = r["bound_model"]
+    return "%.3f of its bound (%s: %.4f ms%s); %.3f of dense FP4 alone" % (
+        r["frac"], r["bound"], bm["bound_ms"],
+        " incl. the agree's bytes" if r.get("agree_fused_in_match") else "",
+        r["fp4_only_view"]["frac"])
 
 
 def lines(name):
@@ -43,8 +44,11 @@ def bench_table():
         d = L[c]
         r = d["roofline"]
         h = r["hbm"]
-        search = "%.4f ms in frame (%.4f back to back), %s; PMC %s%s MB (algorithmic %.1f)" % (
-            r["ms_per_launch"], r["back_to_back"]["ms_per_launch"], bound_text(r),
+        search = "%s %.4f ms in frame%s, %s; PMC %s%s MB (algorithmic %.1f)" % (
+            "search + agree launch" if r.get("agree_fused_in_match") else "search",
+            r["ms_per_launch"],
+            " (search alone %.4f)" % r["search_alone_in_frame"]["ms"] if r.get("agree_fused_in_match")
+            else " (%.4f back to back)" % r["search_alone_in_frame"]["back_to_back_ms"], bound_text(r),
             "search + agree, one launch: " if r.get("agree_fused_in_match") else "",
             "%.1f" % (r["traffic"] / 1e6) if r.get("traffic") else "n/a",
             r.get("algorithmic_bytes_traffic_covers", r["algorithmic_bytes"]) / 1e6)
@@ -59,7 +63,7 @@ def bench_table():
                 d["ms_per_match_one_at_a_time"], d["vs_published"]["speedup"])
         rows.append("| %s | %.0f | %.4f | %s | %s | %.0f%s |" % (
             label, d["value"], d["ms_per_step"], search, other, P0[c]["value"], DRIVER_PREV.get(c, "")))
-    head = ["| config | Mpix/s | ms/step | search stage | other stages (back to back) | round 4 Mpix/s |",
+    head = ["| config | Mpix/s | ms/step | search stage | other stages (back to back) | round 5 Mpix/s |",
             "|---|---|---|---|---|---|"]
     return "\n".join(head + rows)
 
@@ -67,7 +71,7 @@ def bench_table():
 def integ_table():
     A, B = lines(CUR), lines(PREV)
     out = ["| n (bits, set) | one match at a time, ms: no subpixel / 0.25 / 0.20 / 0.15 / 0.10 | "
-           "RTX 4090 ms | × | search ms in frame, frac (bound) | round 4: ×, search ms |",
+           "RTX 4090 ms | × | search ms in frame, frac (bound) | round 5: ×, search ms |",
            "|---|---|---|---|---|---|"]
     for n in (6, 8, 12, 16):
         names = ["integ-n%d" % n] + ["integ-n%d-s%d" % (n, s) for s in (25, 20, 15, 10)]

@@ -27,25 +27,55 @@ SHAPES = {"cfg2": (1536, 2048, 6), "cfg5": (2160, 3840, 6)}  # rows, cols, bytes
 LINK_GBPS = (153.0, 64.0)
 
 
-def load(path):
+def load(path, with_ingress=False):
+    """{(config, N, root_load): median ms_per_step}; with_ingress: also {key: (all steps
+    landed, median achieved ingress GB/s)} from round-6 records (tools/jl.py lines, whose
+    `ingress` holds bench.py's root_load object)."""
     rows = [json.loads(l) for l in open(path) if l.strip()]
-    tab = {}
+    tab, ing = {}, {}
     for r in rows:
-        key = (r["config"], r["band_of"], r["root_load"])
+        key = (r["config"], int(r["band_of"]), r["root_load"])
         tab.setdefault(key, []).append(r["ms_per_step"])
-    return {k: sorted(v)[len(v) // 2] for k, v in tab.items()}
+        g = r.get("ingress")
+        if g:
+            ing.setdefault(key, []).append((g["loads_issued"] == r.get("steps", g["loads_issued"]) and
+                                            not g.get("steps_skipped"), g["ingress_GBps"]))
+    med = {k: sorted(v)[len(v) // 2] for k, v in tab.items()}
+    if not with_ingress:
+        return med
+    return med, {k: (all(a for a, _ in v), sorted(b for _, b in v)[len(v) // 2])
+                 for k, v in ing.items()}
 
 
-def predict(tab, n1):
+def dma_mode(tab, cfg, N):
+    """The copy-engine rehearsal row for an N-way run: streams = the N - 1 senders' copies,
+    at most 4 (round 6 rows dma1 / dma2 / dma4), else round 5's single "dma" row."""
+    k = 1 if N <= 2 else 2 if N <= 4 else 4
+    for m in ("dma%d" % k, "dma"):
+        if (cfg, N, m) in tab:
+            return m
+    return "dma%d" % k
+
+
+def predict(tab, n1, ingress=None):
     out = []
     for (cfg, N, mode), t in sorted(tab.items()):
         if mode != "none" or cfg not in SHAPES:
             continue
         H, W, bpp = SHAPES[cfg]
         band_bytes = -(-H // N) * W * bpp
-        for gather, load_mode in (("rccl", "proxy16"), ("dma", "dma")):
+        for gather, load_mode in (("rccl", "proxy16"), ("dma", dma_mode(tab, cfg, N))):
             tl = tab.get((cfg, N, load_mode))
             slow = (tl / t) if tl else None
+            status = None
+            if ingress is not None and (cfg, N, load_mode) in ingress:
+                # rehearsed only if every step landed its bytes at the rate the band alone
+                # needs (VERDICT r05: else the row is an upper bound, "unrehearsed")
+                landed, gbps = ingress[(cfg, N, load_mode)]
+                need = (N - 1) * band_bytes / (t * 1e-3) / 1e9
+                status = ("rehearsed" if landed and gbps >= 0.95 * need else
+                          "unrehearsed: %s%.0f of the %.0f GB/s the band alone needs" % (
+                              "" if landed else "steps skipped; ", gbps, need))
             for link in LINK_GBPS:
                 t_link = band_bytes / (link * 1e9) * 1e3
                 t_root = t * (slow or 1.0)
@@ -55,6 +85,7 @@ def predict(tab, n1):
                 out.append({"config": cfg, "N": N, "gather": gather, "band_ms": t,
                             "root_slowdown": round(slow, 4) if slow else None,
                             "root_slowdown_source": load_mode if slow else "not measured (1.0)",
+                            "rehearsal": status,
                             "link_GBps": link, "link_ms": round(t_link, 4),
                             "predicted_ms_per_step": round(step, 4),
                             "predicted_Mpix_s": round(mpix, 0),
@@ -64,12 +95,13 @@ def predict(tab, n1):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--profile", default=os.path.join(ROOT, "profiles", "root_gather_r05.jsonl"))
-    ap.add_argument("--n1", default="cfg2=7862,cfg5=4981",
-                    help="measured N = 1 Mpix/s per config (bench.py, 2 frames in flight)")
+    ap.add_argument("--profile", default=os.path.join(ROOT, "profiles", "root_gather_r06.jsonl"))
+    ap.add_argument("--n1", default="cfg2=7740,cfg5=4741",
+                    help="measured N = 1 Mpix/s per config (bench.py at its default frames in flight)")
     args = ap.parse_args()
     n1 = {k: float(v) for k, v in (x.split("=") for x in args.n1.split(","))}
-    for line in predict(load(args.profile), n1):
+    tab, ing = load(args.profile, with_ingress=True)
+    for line in predict(tab, n1, ing):
         print(json.dumps(line))
 
 
