@@ -1628,18 +1628,19 @@ MxGeometry search_mx_geometry(int rows, int cols, int words, int lds_bytes, int 
     }
     // packed keys: the default NoDuplicates search for 32/64-bit descriptors (one K-step,
     // where the key reduction, not the matrix products, bounds the one-product search: FULL
-    // n = 6 0.63 vs 1.43 ms, n = 8 0.78 vs 0.97 ms at 3208x2200, profiles/search_integ_r04.jsonl)
-    // and, since its drops became lazy (round 6), for 128-bit descriptors with <= 127 used
-    // bits too (LIMITED n <= 33, FULL n <= 12): cfg2 0.334 vs 0.349 ms, cfg5 1.364 vs 1.446,
-    // readme 1.073 vs 1.078, random cfg2 0.382 vs 0.481 (profiles/pk128_r06.jsonl; round 3,
-    // with the drop branch, it measured slower: 0.336 vs 0.311 ms, pk_keys_r03.jsonl);
-    // or wherever variant 68 asks for it. Same workgroup shape, a wide tile = two 32-col0
-    // tiles; the LDS stage holds one expanded word per descriptor word
+    // n = 6 0.63 vs 1.43 ms, n = 8 0.78 vs 0.97 ms at 3208x2200, profiles/search_integ_r04.jsonl),
+    // or wherever variant 68 (or BICOS_PK128=1, for 128-bit descriptors with <= 127 used bits)
+    // asks for it. With lazy drops (round 6) the 128-bit packed search is faster back to back
+    // (cfg2 0.334 vs 0.349 ms, random descriptors 0.382 vs 0.481; profiles/pk128_r06.jsonl), but
+    // in the bench's frames it only ties or loses where it matters: cfg2 7889 / 7847 vs 7858 /
+    // 7913 Mpix/s, readme -1.2 %, cfg2's 192-row bands of the 8-GPU run -11 % (one wide tile per
+    // wave), cfg5 +2.4 % -- so the one-product search stays the 128-bit default.
+    // Same workgroup shape, a wide tile = two 32-col0 tiles; the LDS stage holds one expanded
+    // word per descriptor word
     // (32/64-bit words need no used-bits hint: a distance is at most 64 <= PK_MAX_BITS)
-    // (BICOS_PK128=0: the one-product search for 128-bit descriptors again; A/B, read once)
     static const bool pk128 = [] {
         const char* v = std::getenv("BICOS_PK128");
-        return !(v && !std::strcmp(v, "0"));
+        return v && !std::strcmp(v, "1");
     }();
     g.pk = (keys == 4 || (keys == 0 && (words <= 2 || (words == 4 && PK_LAZY && pk128)))) &&
            (words <= 2 || (bits > 0 && bits <= PK_MAX_BITS)) && bits <= 32 * words &&

@@ -1388,3 +1388,30 @@ def test_consistency_dense_rows(gpu, oracle, n, W, kw, nxc):
     same(host(d), rd)
     if rc is not None:
         same(host(c), rc)
+
+
+# ------------------ the 128-bit packed-key search with its fused agree (variant 68 / BICOS_PK128=1)
+# Not the default (it ties or loses in the frames), still a supported tuning:
+# engines tuned to variant 68 run search_pk_kernel<4, ...> with lazy drops and, for cfg2's
+# shapes, the agree inside the same launch. Byte-identical to the default engine's maps; the
+# 192-row band (one wide tile per wave) and a 300-row frame (two) against cfg2's oracle hashes.
+@pytest.mark.parametrize("rows", [192, 300])
+def test_pk128_fused_equals_default(gpu, rows):
+    from libbicos_amd.device import Engine, MatchConfig
+    from tests.golden.make_frames import band_hashes
+    rec = _frames()["cfg2"]
+    n, W = rec["n"], rec["W"]
+    L, R = _frame_stacks(n, rec["H"], W)
+    s0, s1 = dev(L[:, :rows]), dev(R[:, :rows])
+    cfg = MatchConfig(**rec["config"])
+    e68 = Engine(0)
+    e68.tune(68)
+    plan = e68.plan(s0, s1, cfg)
+    assert plan & _lib.PLAN_PACKED_KEYS and plan & _lib.PLAN_AGREE_IN_SEARCH
+    d, c = e68.match(s0, s1, cfg)
+    dd, dc = gpu.match(s0, s1, cfg)
+    same(host(d), host(dd))
+    same(host(c), host(dc))
+    if rows == 192:
+        assert band_hashes(host(d), 64) == rec["disparity_bands"][:3]
+        assert band_hashes(host(c), 64) == rec["corrmap_bands"][:3]
