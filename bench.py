@@ -540,6 +540,27 @@ def main():
         if dma is None and want_dma and not nccl:
             # (the rccl-form rehearsal over gloo moves host buffers)
             raise SystemExit("--gather dma setup failed on a gloo rehearsal")
+        gather_choice = None
+        if dma is not None and nccl and args.gather == "auto":
+            # auto (round 6): both gathers timed alone before anything is timed; the
+            # copy-engine one is kept unless it is slower than 1.25 x the RCCL gather. One GPU
+            # cannot rehearse it at rate (profiles/root_gather_r06.jsonl: HBM-to-HBM copy
+            # engines reach 34-135 GB/s of the 50-301 GB/s rank 0 needs), and
+            # its advantage -- nothing on rank 0's compute units -- is worth a slower transfer
+            # only up to a point
+            t_dma = time_dma_exchange(dist, torch, dev, rank, world, dma, streams[0], nbytes, reps=5)
+            t_rccl = time_gather(dist, torch, dev, nccl, rank, sends[0], recvs[0], nbytes, world,
+                                 reps=5)
+            tt = torch.tensor([t_rccl["ms"]], dtype=torch.float64, device=dev)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            ms_rccl = float(tt.item())
+            keep = t_dma["ms_per_exchange"] <= 1.25 * ms_rccl
+            gather_choice = {"dma_ms_per_exchange": t_dma["ms_per_exchange"],
+                             "rccl_ms_per_gather": round(ms_rccl, 4),
+                             "rule": "dma unless its exchange takes > 1.25 x the RCCL gather",
+                             "chosen": "dma" if keep else "rccl"}
+            if not keep:
+                dma = None
         # rank 0: the float32 disparity frame of each gather slot (one per slot,
         # so a stale or misordered landing cannot hide behind a shared buffer)
         frame_disps = [torch.empty((world, hb, W), dtype=torch.float32, device=gdev)
@@ -723,6 +744,8 @@ def main():
     # ---- after the timed region: the gather alone, then the gathered frames verified
     gather_info = None
     verify = None
+    if not gather:
+        gather_choice = None
     if gather:
         if dma is not None:
             gather_info = time_dma_exchange(dist, torch, dev, rank, world, dma, streams[0], nbytes)
@@ -732,7 +755,9 @@ def main():
         else:
             gather_info = time_gather(dist, torch, dev, nccl, rank, sends[0], recvs[0], nbytes, world)
             if want_dma and nccl:
-                gather_info["dma_exchange"] = "unavailable: the copy-engine setup failed"
+                gather_info["dma_exchange"] = (
+                    "not chosen: %s" % json.dumps(gather_choice) if gather_choice
+                    else "unavailable: the copy-engine setup failed")
         if not args.no_verify_gather:
             verify = verify_gather(args, C, dist, torch, np, dev, nccl, rank, world, eng, mcfg,
                                    step, drain, NB, recv_all, frame_disps, disp_view, corr_view,
@@ -814,6 +839,7 @@ def main():
             },
             "roofline": roof,
             "gather": gather_info,
+            "gather_choice": gather_choice,
             "root_load": None if load is None else {
                 "mode": load["mode"], "bytes_per_step": load["bytes_per_step"],
                 "loads_issued": load["issued"], "steps_skipped": load["skipped"],

@@ -1,13 +1,13 @@
 #!/bin/bash
 # Frames in flight at N = 1: F = FLS (default 1 2 3) interleaved per config,
-# ROUNDS passes, at the driver's default step count (20) and a longer one (STEPS2). One JSON
+# ROUNDS passes, at the driver's default step count (20) and a longer one (STEPSLIST). One JSON
 # line per run in gpurun_out/inflight_r06.jsonl. Stops at the first crash / timeout.
 set -u
 mkdir -p gpurun_out
-out=gpurun_out/inflight_r06.jsonl
+out=${OUT:-gpurun_out/inflight_r06.jsonl}
 for r in $(seq ${ROUNDS:-2}); do
   for c in ${SCS:-cfg1 cfg2 cfg3 cfg4 cfg5}; do
-    for steps in 20 ${STEPS2:-200}; do
+    for steps in ${STEPSLIST:-20 200}; do
       for f in ${FLS:-1 2 3}; do
         timeout -k 10 120 python bench.py --config $c --inflight $f --steps $steps --warmup 3 \
             --no-cpu-baseline --no-host-path --kernel-reps 0 > gpurun_out/ifl.txt 2> gpurun_out/ifl.err

@@ -20,6 +20,12 @@ for step in "$@"; do
       tail -1 gpurun_out/smoke.txt ;;
     inflight)
       bash tools/inflight_ab.sh || exit 1 ;;
+    sdma)
+      timeout -k 10 120 python tools/sdma_probe.py --out gpurun_out/sdma_probe_r06.jsonl > gpurun_out/sdma.txt 2>&1 \
+        || { tail gpurun_out/sdma.txt; exit 1; } ;;
+    inflight2)  # the reference-shaped configs (README / integration grid), F = 1 / 2 at 20 steps
+      SCS="readme integ-n6 integ-n8 integ-n12 integ-n16 integ-n12-s25" FLS="1 2" STEPSLIST=20 \
+        OUT=gpurun_out/inflight2_r06.jsonl bash tools/inflight_ab.sh || exit 1 ;;
     mfma)
       timeout -k 10 200 ./build/mfma_rate > gpurun_out/mfma_r06.txt 2>&1 || exit 1
       cat gpurun_out/mfma_r06.txt ;;
