@@ -12,7 +12,7 @@ step k overlaps the kernels of step k+1 (double-buffered), and every gather has
 completed before the closing barrier.
 
 Frames in flight (--inflight F; on one GPU per config -- 1 for cfg2 / cfg4 / cfg5, 2 for
-cfg1 / cfg3 -- and 6 for row bands on N > 1): step k runs on stream k % F with its own
+cfg1 / cfg3 / readme / integ-* -- and 6 for row bands on N > 1): step k runs on stream k % F with its own
 engine and output buffers, so consecutive frames overlap the way a camera stream is
 processed -- the HBM-bound transform / agree of one frame fill the compute-unit slots the
 previous frame's search leaves idle in its last round of workgroups (narrow row bands:
@@ -121,12 +121,15 @@ del _n, _s, _ms, _cfg
 # one session at the driver's 20 steps and at 200 (profiles/inflight_r06.jsonl). A config
 # keeps 2 only where 2 won by more than the run-to-run spread (~1.3 %): cfg1 (launch-bound:
 # 13030 vs 9729 Mpix/s at F = 1), cfg3 (the subpixel refine overlaps the next frame's search:
-# +2.6 %). cfg2 / cfg4 / cfg5: F = 1 (cfg2 7740 vs 7668 at 20 steps, 7751 vs 7824 at 200;
-# cfg5 4741 vs 4693). Other configs: 1, unless listed.
-INFLIGHT_DEFAULT = {"cfg1": 2, "cfg3": 2}
+# +2.6 %), readme (+1.9 %) and the integration grid (FULL n = 6 / 8 / 12 / 16 +5.9 / +2.7 /
+# +1.3 / +1.5 %, n = 12 with subpixel +2.2 %). cfg2 / cfg4 / cfg5: F = 1 (cfg2 7740 vs 7668
+# at 20 steps, 7751 vs 7824 at 200; cfg5 4741 vs 4693).
+INFLIGHT_DEFAULT = {"cfg1": 2, "cfg3": 2, "readme": 2}
 
 
 def inflight_default(config: str) -> int:
+    if config.startswith("integ-"):
+        return 2
     return INFLIGHT_DEFAULT.get(config, 1)
 
 
@@ -363,7 +366,8 @@ def main():
                     help="frames in flight: step k runs on stream k %% F with its own engine, so "
                          "one frame's HBM-bound stages fill the slots the previous frame's "
                          "search leaves idle (1 = strictly one match after another). Default on "
-                         "one GPU: per config (INFLIGHT_DEFAULT: 2 for cfg1 / cfg3, else 1; "
+                         "one GPU: per config (INFLIGHT_DEFAULT: 2 for cfg1 / cfg3 / readme / the "
+                         "integration grid, else 1; "
                          "profiles/inflight_r06.jsonl), 6 for N > 1 row bands and --band-of "
                          "(band 0 of 8: cfg5 0.2140-0.2146 vs 0.2244-0.2281 ms with 3, cfg2 within "
                          "1 %%; profiles/bands_inflight_r05.jsonl)")
