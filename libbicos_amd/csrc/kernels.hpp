@@ -81,10 +81,6 @@ struct SearchArgs {
 struct SearchAgreeArgs {
     SearchArgs s;
     AgreeArgs ag;
-    // experiment (BICOS_AG_STAGGER): workgroups [stagger_lo, stagger_hi) of the
-    // first round sleep stagger_sleeps x s_sleep 127 before starting, so the two workgroups of
-    // a CU run their agree phases out of step; 0 = off
-    int stagger_lo, stagger_hi, stagger_sleeps;
 };
 
 struct SearchGeometry {

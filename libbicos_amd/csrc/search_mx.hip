@@ -477,10 +477,6 @@ template <int WORDS, int KSU, bool NODUPES, int T, int KEYS, bool TAIL, bool LIS
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(KSU >= 4 ? 3 : 4)))
 void search_mx_kernel(typename SearchKArgs<AG>::type ka) {
     const SearchArgs& a = search_part(ka);
-    if constexpr (AG) {
-        if (ka.stagger_sleeps && (int)blockIdx.x >= ka.stagger_lo && (int)blockIdx.x < ka.stagger_hi)
-            for (int i = 0; i < ka.stagger_sleeps; ++i) __builtin_amdgcn_s_sleep(127);
-    }
     constexpr bool FK = KEYS == 3;
     static_assert(!FK || !NODUPES, "FK keys: first minimum only");
     constexpr bool XK = KEYS == 1 || KEYS == 2;
@@ -1385,22 +1381,10 @@ void search_pk_kernel(typename SearchKArgs<AG>::type ka) {
 // kernel arguments of a launch: the search's, plus the agree's for AG
 template <bool AG>
 typename SearchKArgs<AG>::type kernel_args(const SearchArgs& a, const AgreeArgs* ag) {
-    if constexpr (AG) {
-        // BICOS_AG_STAGGER=<sleeps>[:<cus>] (experiment, read once): the second half of the
-        // first round of workgroups (2 per CU) starts late
-        static const int sleeps = [] {
-            const char* v = std::getenv("BICOS_AG_STAGGER");
-            return v ? std::atoi(v) : 0;
-        }();
-        static const int cus = [] {
-            const char* v = std::getenv("BICOS_AG_STAGGER");
-            const char* c = v ? std::strchr(v, ':') : nullptr;
-            return c ? std::atoi(c + 1) : 256;
-        }();
-        return SearchAgreeArgs{a, *ag, cus, 2 * cus, sleeps};
-    } else {
+    if constexpr (AG)
+        return SearchAgreeArgs{a, *ag};
+    else
         return a;
-    }
 }
 
 // Lazy drops pay a fixed rescan per col0 (~32 popcounts of WORDS words); the drop branch

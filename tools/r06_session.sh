@@ -20,12 +20,6 @@ for step in "$@"; do
       tail -1 gpurun_out/smoke.txt ;;
     inflight)
       bash tools/inflight_ab.sh || exit 1 ;;
-    abstagger)  # fused search + agree: the first round's second workgroups per CU start late
-      for k in 1 2; do for v in 0 4 7 10; do for c in cfg2 cfg5; do
-        BICOS_AG_STAGGER=$v timeout -k 10 200 python bench.py --config $c --steps 40 --warmup 3 --no-cpu-baseline \
-          --no-host-path --kernel-reps 10 2> gpurun_out/abst.err | python tools/jl.py gpurun_out/abstagger_r06.jsonl \
-          stagger=$v round=$k || { tail gpurun_out/abst.err; exit 1; }
-      done; done; done ;;
     sdma)
       timeout -k 10 120 python tools/sdma_probe.py --out gpurun_out/sdma_probe_r06.jsonl > gpurun_out/sdma.txt 2>&1 \
         || { tail gpurun_out/sdma.txt; exit 1; } ;;
