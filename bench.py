@@ -255,6 +255,18 @@ def mx_key_pair_peak(words: int, cfg: dict, reach: float = MX_REACH_PLANTED) -> 
     return 1024.0 / per_unit_s
 
 
+def lr_key_pair_peak() -> float:
+    """Issue bound in pairs/s of the one-pass Consistency search's VALU (search_mx.hip
+    search_lr_kernel), from its ISA per wave and block of 2 tiles x 32 col1 =
+    2048 pairs: forward 16 v_min3_f32 (half rate) + 2 v_add_f32; reverse 16 v_min_u32 (the tile
+    pair), 8 v_permlane16_swap + 8 v_min_u32, 7 v_min_u32_dpp + 1 v_min_u32 (half), 14
+    v_cndmask + v_mov_dpp + v_add_f32 (full), 4 LDS-address v_add_u32 (full): 56 half-rate and
+    22 full-rate lane-ops per lane."""
+    half = 56.0 * 64 / 2048
+    full = 22.0 * 64 / 2048
+    return 1.0 / (half / (VALU_HALF_TOPS * 1e12) + full / (VALU_FULL_TOPS * 1e12))
+
+
 def mx_key_pair_peak_all_trees() -> float:
     """The round-5 key-reduction model (both trees on every pair: 1 v_xor + 1 v_min3 per
     pair), kept as the upper-bound view VERDICT r05 quoted (25.1 Tpairs/s)."""
@@ -1131,9 +1143,11 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     st_corr = torch.empty((rows, W), dtype=torch.float64 if mcfg.precision else torch.float32,
                           device=dev) if has_corr else None
 
+    one_pass = bool(plan & getattr(_lib, "PLAN_CONSISTENCY_ONE_PASS", 0))
+
     def search_launch():
-        # with the used-bits hint the pipeline passes (engine.cpp match_device)
-        eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw, bits=ubits)
+        # with the set-bits hint the pipeline passes (engine.cpp match_device)
+        eng.search(d0, d1, W, words, flags, mcfg.max_lr_diff, out=raw, bits=sbits)
 
     def stage_launch():  # the match past its transform (bicos_search_agree_device)
         eng.search_agree(d0, d1, s0, s1, mcfg, out=st_out, corrmap=st_corr)
@@ -1192,20 +1206,26 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
     # the disparity, 6 B per pixel)
     search_bytes = rows * W * (2 * 4 * words + 2) * (2 if mc.get("variant", 0) == 1 else 1) + \
         (rows * W * 6 if mc.get("variant", 0) == 1 else 0)
+    if one_pass:  # one launch: both descriptor bands in, the checked disparity out
+        search_bytes = rows * W * (2 * 4 * words + 2)
     mx = mx_search()
     cons = mc.get("variant", 0) == 1
     nodupes = not cons or bool(mc.get("no_dupes", False))
     pk = bool(plan & _lib.PLAN_PACKED_KEYS)
     kname = ("search_pk_kernel" if pk else "search_mx_kernel") if mx else "search16_kernel"
+    if one_pass:
+        kname = "search_lr_kernel"
     cfgname = args.config
     # the search stage's bytes per frame: every search dispatch (tail launches, both
     # Consistency passes, the reverse list) and Consistency's check kernel
-    traffic = load_traffic((kname, "consistency_kernel") if cons else kname,
+    traffic = load_traffic((kname, "consistency_kernel") if cons and not one_pass else kname,
                            cfgname, rows)
     # Consistency: the distinct col1 the forward search keeps, over which the reverse search
     # runs (engine.cpp reverse_search)
     kept = None
-    if cons and mx:
+    if one_pass:
+        kept = 0.0  # the reverse search reuses the forward products: no pairs of its own
+    elif cons and mx:
         fwd = torch.empty_like(raw)
         eng.search(d0, d1, W, words, 1 if nodupes else 0, -1, out=fwd, bits=ubits)
         c0 = torch.arange(W, device=dev, dtype=torch.int64).expand(rows, W)
@@ -1221,7 +1241,8 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
                                      mark[:, :W].sum(dim=1)).sum().item())
     if mx:
         alg_flops, used_flops = mx_flops(rows, W, words, mc, ubits, sbits, reverse_col1=kept)
-        kpeak = (pk_key_pair_peak() if pk else mx_key_pair_peak(words, mc, mx_reach_planted(W))) / 1e9
+        kpeak = (lr_key_pair_peak() if one_pass else pk_key_pair_peak() if pk else
+                 mx_key_pair_peak(words, mc, mx_reach_planted(W))) / 1e9
         evaluated = pairs + (kept if kept is not None else pairs / W) * W if cons else pairs
         k_exec = int(round(alg_flops / (2 * evaluated)))
         # the launch the line is about: the fused search + agree (the match's own launch) or
@@ -1237,7 +1258,11 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
                "frac": round(achieved_tf / MFMA_FP4_DENSE_TFLOPS, 4)}
         kview = {"achieved": round(evaluated / t_main / 1e9, 1), "peak": round(kpeak, 1),
                  "unit": "Gpairs/s", "frac": round(t_key / t_main, 4)}
-        if fused:
+        if one_pass:
+            kname_long = ("search_lr_kernel<%d words> (Consistency in one launch: the forward and "
+                          "the reverse FP4 MFMA Hamming argmin from one set of products, the "
+                          "left-right check in the same workgroup)" % words)
+        elif fused:
             kname_long = ("search_pk_kernel<1 word, AG> (packed-key FP4 MFMA search with the NXC "
                           "agree of its col0 in the same launch)" if pk else
                           "search_mx_kernel<%d words, AG> (FP4 MFMA Hamming argmin with the NXC "
@@ -1270,7 +1295,9 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
                 "key_reduction_ms": round(t_key * 1e3, 4),
                 "agree_hbm_ms": round(t_ag * 1e3, 4),
                 "bound_ms": round(t_bound * 1e3, 4),
-                "key_model": ("pk_key_pair_peak: 10 half-rate + 1 full-rate lane-ops per lane, wide "
+                "key_model": ("lr_key_pair_peak: 56 half-rate + 22 full-rate lane-ops per lane and "
+                              "block of 2 tiles (both directions' reductions)" if one_pass else
+                              "pk_key_pair_peak: 10 half-rate + 1 full-rate lane-ops per lane, wide "
                               "tile and block" if pk else
                               "mx_key_pair_peak: the ISA's VALU per (wave, tile, block), the "
                               "last-minimum tree weighted by the planted frame's reach fraction "

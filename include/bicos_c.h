@@ -246,6 +246,7 @@ int bicos_agree_stage_device(const int16_t* raw, const void* stack0, const void*
 #define BICOS_PLAN_REVERSE_COMPACTED 8      /* Consistency: reverse search over kept col1 */
 #define BICOS_PLAN_CONSISTENCY_IN_AGREE 16  /* Consistency: left-right check in the agree */
 #define BICOS_PLAN_DENSE_ROWS 32            /* ... rows kept >= 7/8 skip the entry prologue */
+#define BICOS_PLAN_CONSISTENCY_ONE_PASS 64  /* Consistency: both searches + the check, one launch */
 int bicos_match_plan(bicos_engine* e, const void* stack0, const void* stack1, int n, int rows,
                      int cols, size_t row_pitch, size_t plane_pitch, int depth,
                      const BicosConfig* cfg, int has_nxcorr);

@@ -69,6 +69,7 @@ PLAN_AGREE_IN_SEARCH = 4
 PLAN_REVERSE_COMPACTED = 8
 PLAN_CONSISTENCY_IN_AGREE = 16
 PLAN_DENSE_ROWS = 32
+PLAN_CONSISTENCY_ONE_PASS = 64
 
 
 def build(verbose: bool = False, jobs: int = 4) -> str:

@@ -199,6 +199,20 @@ static bool dense_rows() {
     }();
     return on;
 }
+// Consistency without NoDuplicates in one launch where the descriptors allow it (search_mx.hip
+// search_lr_kernel: the forward and reverse searches share their matrix products, the check
+// runs in the same workgroup). BICOS_LR_ONE_PASS=0: the two searches + the check (A/B; read
+// per call, so one process can compare the two forms).
+static bool lr_one_pass() {
+    const char* v = std::getenv("BICOS_LR_ONE_PASS");
+    return !(v && !std::strcmp(v, "0"));
+}
+// Descriptor bits the transform writes, exactly (descriptor_transform.hpp:31-123; used_bits
+// is an upper bound): LIMITED 4n-6 for n >= 4 (7 for n = 3, 4 for n = 2), FULL n^2-2n+3
+static int written_bits(int n, int mode) {
+    if (mode) return n * n - 2 * n + 3;
+    return n >= 4 ? 4 * n - 6 : (n == 3 ? 7 : 4);
+}
 // bytes per row of the per-tile valid counts
 static size_t valid_pitch(int cols) { return ((size_t)(cols + 31) / 32 + 15) / 16 * 16; }
 
@@ -242,6 +256,9 @@ int match_plan(const bicos_engine* e, int n, int rows, int cols, size_t row_pitc
             bicos_hip::search_mx_agree_fusable(g, words, true, cols, n, depth, dbl))
             plan |= BICOS_PLAN_AGREE_IN_SEARCH;
     }
+    if (consistency && mx && !nodupes && lr_one_pass() &&
+        bicos_hip::search_lr_eligible(words, written_bits(n, mode), cols))
+        return plan | BICOS_PLAN_CONSISTENCY_ONE_PASS;
     if (consistency) {
         if (reverse_compacted(mx)) {
             plan |= BICOS_PLAN_REVERSE_COMPACTED;
@@ -303,7 +320,8 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     const size_t map16 = align_up((size_t)rows * cols * 2);
     const size_t vpitch = valid_pitch(cols);
     const size_t vbytes = (plan & BICOS_PLAN_DENSE_ROWS) ? align_up((size_t)rows * vpitch) : 0;
-    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) + (consistency ? 2 * map16 : 0) + vbytes;
+    const bool two_maps = consistency && !(plan & BICOS_PLAN_CONSISTENCY_ONE_PASS);
+    size_t need = 2 * desc_bytes + (has_nxcorr ? map16 : 0) + (two_maps ? 2 * map16 : 0) + vbytes;
     int rc = reserve(e->ws, e->ws_bytes, need, e->device, st, e->ws_ready);
     if (rc) return rc;
     // order against earlier users of ws / stage on other streams; mark our use on exit
@@ -321,8 +339,8 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
     p += desc_bytes;
     int16_t* raw = has_nxcorr ? (int16_t*)p : (int16_t*)disp;
     if (has_nxcorr) p += map16;
-    int16_t* fwd = consistency ? (int16_t*)p : nullptr;
-    int16_t* rev = consistency ? (int16_t*)(p + map16) : nullptr;
+    int16_t* fwd = two_maps ? (int16_t*)p : nullptr;
+    int16_t* rev = two_maps ? (int16_t*)(p + map16) : nullptr;
     uint8_t* valid = vbytes ? (uint8_t*)(p + 2 * map16) : nullptr;  // dense-row fast path
 
     // 1. descriptor_transform, both stacks in one launch (cpu.cpp:50-59)
@@ -380,7 +398,12 @@ int match_device(bicos_engine* e, const void* s0, const void* s1, int n, int row
         return check_hip(bicos_hip::launch_search_mx_agree(sa, aa, g, st), "search + agree launch");
     }
 
-    if (!consistency) {
+    if (plan & BICOS_PLAN_CONSISTENCY_ONE_PASS) {
+        bicos_hip::SearchArgs sa{d0, d1, raw, rows, cols, dpitch, (size_t)cols, 0, 0, 0, 0};
+        rc = check_hip(bicos_hip::launch_search_lr(sa, words, written_bits(n, mode), cfg.max_lr_diff, st),
+                       "consistency search launch");
+        if (rc) return rc;
+    } else if (!consistency) {
         rc = search(d0, d1, raw, 0, true, "search launch");
         if (rc) return rc;
     } else {
@@ -1009,6 +1032,11 @@ int bicos_search_device(bicos_engine* e, const uint32_t* desc0, const uint32_t* 
                                                          words, nodupes, st),
                              "search launch");
         return check_hip(bicos_hip::launch_search(sa, g, words, nodupes, st), "search launch");
+    }
+    if (mx && !nodupes && lr_one_pass() && bicos_hip::search_lr_eligible(words, bits, cols)) {
+        bicos_hip::SearchArgs sa{desc0, desc1, out, rows, cols, dpitch, (size_t)cols, 0, 0, 0};
+        return check_hip(bicos_hip::launch_search_lr(sa, words, bits, max_lr_diff, st),
+                         "consistency search launch");
     }
     if (!e) return fail(BICOS_E_ARG, "consistency search needs an engine workspace");
     std::lock_guard<std::mutex> lk(e->lock);  // the workspace may be shared (default engine)

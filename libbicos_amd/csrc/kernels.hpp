@@ -152,6 +152,13 @@ bool search_mx_agree_fusable(const MxGeometry& g, int words, bool nodupes, int c
                              int depth, bool dbl);
 hipError_t launch_search_mx_agree(SearchArgs a, const AgreeArgs& ag, const MxGeometry& g,
                                   hipStream_t st);
+// Consistency in one pass (search_mx.hip search_lr_kernel): the forward and the reverse
+// search from the same matrix products and the left-right check (reference bicos.hpp:78-113,
+// no NoDuplicates), one workgroup per row; a.out gets consistency_kernel's disparity map
+// (out_mode 0). Only 256-bit descriptors with 129..154 used bits (`bits`: their count; the
+// bits above must be zero) and rows of at most 2048 columns: search_lr_eligible.
+bool search_lr_eligible(int words, int bits, int cols);
+hipError_t launch_search_lr(SearchArgs a, int words, int bits, int max_lr_diff, hipStream_t st);
 hipError_t launch_agree(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
 hipError_t launch_subpixel(const AgreeArgs& a, int depth, bool dbl, hipStream_t st);
 // n > 40 (subpixel_wide.hip); launch_subpixel dispatches to it

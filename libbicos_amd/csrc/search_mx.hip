@@ -966,6 +966,280 @@ void search_mx_kernel(typename SearchKArgs<AG>::type ka) {
 }
 
 // ---------------------------------------------------------------------------------------
+// Consistency in one pass (round 6): the forward AND the reverse search from the same matrix
+// products, then the left-right check, one workgroup per row (reference bicos.hpp:78-113;
+// the Consistency variant without NoDuplicates, first minimum both ways).
+//
+// The forward search reduces each D tile along col1 (16 registers of a lane: 8 v_min3); the
+// reverse search needs the same pairs reduced along col0, which the accumulator spreads over
+// the 32 lanes of a half-wave. Two launches (forward, then the reverse over the kept col1)
+// multiply every pair twice; here the products are shared and the reverse reduction costs a
+// lane transposition per block (lr_reduce: 8 v_permlane16_swap + 30 VALU for 32 col1 x the
+// wave's 64 col0) instead of a second set of MFMAs.
+//
+// Keys. The reverse order needs ham itself (|a| varies with col0) and the col0 at the
+// minimum; the forward order needs the col1. All three ride in the products, so that
+//     D = ham(col0, col1) + (col1 % 32) * 2^-12 + (col0 - c0_wave) * 2^-15
+// exactly (ham <= 154, D < 256: 2^-15 is above the ulp):
+//  * |a| (popcount of the left descriptor) in the 6 free K elements of the last K-step's
+//    lower half (descriptor bits 26..31 of word 2 KS - 2, zero for <= 64 KS - 38 used bits):
+//    right (A) constants 1, 6, 6, 6, 6, 6, left (B) FP4 digits with sum = |a| (lr_abs_digits);
+//  * col1 % 32 as KEYS 3 (fk_digits in the upper half's A, B = 2.0, the half scaled 2^-13);
+//  * col0 - c0_wave = 2 j + t in 6 more upper-half elements: A constants 0.5, 0.5, 0.5, 0.5, 1,
+//    2, B = bit k ? 0.5, 1, 2, 4, 4, 4 : 0 (products 2^-2 .. 2^3, x 2^-13).
+// Forward: col0 fixed, so D orders by ham, then col1 (the first minimum); the running minimum
+// is kept relative to the block base exactly as KEYS 3. Reverse: col1 fixed, so D orders by
+// ham, then col0: the tile pair's v_min, the lane transposition, + c0_wave * 2^-15 (exact), and
+// one ds_min_u32 per col1 into the row's LDS array (D >= 0: the bits order like the float).
+// Left columns past the image carry |a| digits of 186 > any distance, so they never win.
+// col0 of wave w in pass p: c0_wave + 2 j + t, c0_wave = (p waves + w) * 64 (interleaved, so
+// the 6-bit col0 offset is the lane and the tile). Passes cover the row; the right row is
+// re-expanded per pass (~2 % of the VALU). The epilogue reads fwd[col0] and rev[fwd[col0]]
+// from LDS and writes consistency_kernel's disparity (reference bicos.hpp:99-106).
+constexpr int LR_MAX_COLS = FK_MAX_COLS;
+constexpr int LR_SA_HI = 127 - 13;              // E8M0 2^-13: the upper half of the last step
+constexpr float LR_C0_EPS = 1.f / 32768.f;      // col0 * 2^-15
+constexpr uint32_t LR_A_W1 = 0x04211110u;       // col0 digit constants, nibbles 1..6 of dword 1
+constexpr uint32_t LR_B_W0 = 0x44444444u;       // 2.0 against the col1 digits (dword 0 ...
+constexpr uint32_t LR_B_W1 = 0x4u;              // ... and nibble 0 of dword 1)
+constexpr uint32_t LR_A_ABS1 = 0x72000000u;     // |a| constants 1, 6 (top byte of dword 1)
+constexpr uint32_t LR_A_ABS23 = 0x77000000u;    // 6, 6 (dwords 2 and 3)
+constexpr int LR_FREE_BITS = 38;                // 32 upper-half + 6 lower-half K elements
+
+// FP4 code of u / 2 for u in {0, 1, 2, 3, 4, 6, 8, 12}
+__device__ __forceinline__ uint32_t lr_code(int u) {
+    return u <= 4 ? (uint32_t)u : (u == 6 ? 5u : (u == 8 ? 6u : 7u));
+}
+// left digits of |a| = n: the top bytes of dwords 1..3 (elements e0..e5, constants 1, 6, ..., 6)
+// with n = v0 + 6 (u1 + .. + u5) / 2: v0 = n % 3, q = n / 3 <= 51 as up to four 12s and the
+// rest in at most two of {0, 1, 2, 3, 4, 6, 8}. n < 0: the past-the-image column, 186.
+__device__ __forceinline__ void lr_abs_digits(int n, uint32_t& b1, uint32_t& b2, uint32_t& b3) {
+    if (n < 0) {
+        b1 = b2 = b3 = 0x77u;
+        return;
+    }
+    const int v0 = n % 3, q = n / 3;
+    const int a = min(4, q / 12), r = q - 12 * a;
+    uint32_t cq = 0;  // nibbles of u1..u5
+    for (int i = 0; i < a; ++i) cq |= 7u << (4 * i);
+    if (a == 4) {
+        cq |= lr_code(r) << 16;
+    } else {
+        const int r1 = r >= 8 ? 8 : (r == 7 ? 6 : (r == 5 ? 4 : r));
+        cq |= lr_code(r1) << (4 * a);
+        cq |= lr_code(r - r1) << (4 * a + 4);
+    }
+    b1 = (uint32_t)(2 * v0) | ((cq & 0xFu) << 4);  // v0 in {0, 1, 2}: codes 0, 2, 4
+    b2 = (cq >> 4) & 0xFFu;
+    b3 = (cq >> 12) & 0xFFu;
+}
+
+// The reverse reduction of one block: v[r] = this lane's key for accumulator row r (col1 =
+// rrow(r) in its half) and col0 = its lane; returns, per lane, the minimum over the 32 lanes
+// of its half of one register's keys (each register's on two adjacent lanes; which register:
+// run it on the rows, lr_rows). Steps: rows 0/1 of a half by v_permlane16_swap, then within
+// 16-lane rows: lanes 8 apart (row_ror:8), mirrored within 8 (row_half_mirror), 2 apart and 1
+// apart (quad_perm), each pairing two registers so that one v_min serves both halves.
+template <int CTRL>
+__device__ __forceinline__ uint32_t lr_mov(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, true);
+}
+__device__ __forceinline__ uint32_t lr_reduce(const uint32_t (&v)[16], int lane) {
+    uint32_t q[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const auto sw = __builtin_amdgcn_permlane16_swap(v[2 * i], v[2 * i + 1], false, false);
+        q[i] = min((uint32_t)sw[0], (uint32_t)sw[1]);
+    }
+    const bool lo8 = (lane & 8) == 0, lo4 = (lane & 4) == 0, lo2 = (lane & 2) == 0;
+    uint32_t w[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t u = lo8 ? q[2 * k] : q[2 * k + 1], x = lo8 ? q[2 * k + 1] : q[2 * k];
+        w[k] = min(u, lr_mov<0x128>(x));  // row_ror:8
+    }
+    uint32_t z[2];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t u = lo4 ? w[2 * k] : w[2 * k + 1], x = lo4 ? w[2 * k + 1] : w[2 * k];
+        z[k] = min(u, lr_mov<0x141>(x));  // row_half_mirror
+    }
+    const uint32_t u = lo2 ? z[0] : z[1], x = lo2 ? z[1] : z[0];
+    const uint32_t y = min(u, lr_mov<0x4E>(x));  // quad_perm [2, 3, 0, 1]
+    return min(y, lr_mov<0xB1>(y));             // quad_perm [1, 0, 3, 2]
+}
+
+template <int WORDS, int KS>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
+void search_lr_kernel(SearchArgs a, int max_lr_diff) {
+    constexpr int T = 2;
+    constexpr int WL = 2 * KS;
+    static_assert(2 * KS <= WORDS, "K-steps exceed the descriptor");
+    extern __shared__ __attribute__((aligned(16))) v4i lds_mx[];  // [WL][chunk] | rev | fwd
+    const int row = blockIdx.x;
+    if (row >= a.rows) return;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int h = lane >> 5;
+    const int j = lane & 31;
+    const int cols = a.cols;
+    const int chunk = a.chunk;
+    const int waves = blockDim.x >> 6;
+    const int cols32 = (cols + 31) & ~31;
+    uint32_t* rev = reinterpret_cast<uint32_t*>((char*)lds_mx + (size_t)WL * chunk * 16);
+    int16_t* fwd = reinterpret_cast<int16_t*>(rev + cols32);
+    for (int i = threadIdx.x; i < cols32; i += blockDim.x) rev[i] = 0xFFFFFFFFu;
+
+    const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
+    const uint32_t* __restrict__ row1 = a.desc1 + (size_t)row * a.desc_pitch;
+    auto rrow = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; };
+    // the block-relative col1 whose reverse key lr_reduce leaves in this lane
+    int rc1;
+    {
+        uint32_t v[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = (uint32_t)rrow(r);
+        rc1 = (int)lr_reduce(v, lane);
+    }
+    const int sa_hi = h ? LR_SA_HI : 127;
+    const int per_pass = waves * T * 32;
+    const int passes = (cols + per_pass - 1) / per_pass;
+    const int nchunks = (cols + chunk - 1) / chunk;
+    for (int pass = 0; pass < passes; ++pass) {
+        const int c0_wave = (pass * waves + wave) * (T * 32);
+        const bool idle = c0_wave >= cols;  // wave-uniform; still joins the barriers
+        // B fragments: +1 (0x2) where the left bit is 0, -1 (0xA) where it is 1, then the
+        // digits of |a| (lower half) and the col1 / col0 digit columns (upper half)
+        v4i bf[T][KS];
+#pragma unroll
+        for (int t = 0; t < T; ++t) {
+            const int c0 = c0_wave + 2 * j + t;
+            const bool in = c0 < cols;
+            int pc = 0;
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const int w = 2 * s + h;
+                const uint32_t x = in ? row0[(size_t)c0 * WORDS + w] : 0u;
+                pc += __popc(x);
+                bf[t][s] = expand_bits(x, LUT_B);
+            }
+            pc += __shfl_xor(pc, 32);  // both halves' words: |a|
+            if (h == 0) {
+                uint32_t b1, b2, b3;
+                lr_abs_digits(in ? pc : -1, b1, b2, b3);
+                v4i& f = bf[t][KS - 1];
+                f[1] = (int)(((uint32_t)f[1] & 0x00FFFFFFu) | (b1 << 24));
+                f[2] = (int)(((uint32_t)f[2] & 0x00FFFFFFu) | (b2 << 24));
+                f[3] = (int)(((uint32_t)f[3] & 0x00FFFFFFu) | (b3 << 24));
+            } else {
+                const uint32_t c0w = (uint32_t)(2 * j + t);
+                uint32_t w1 = LR_B_W1;
+                constexpr uint32_t code[6] = {0x1u, 0x2u, 0x4u, 0x6u, 0x6u, 0x6u};
+#pragma unroll
+                for (int k = 0; k < 6; ++k)
+                    if (c0w & (1u << k)) w1 |= code[k] << (4 * (k + 1));
+                bf[t][KS - 1] = v4i{(int)LR_B_W0, (int)w1, 0, 0};
+            }
+        }
+        float m1[T];
+#pragma unroll
+        for (int t = 0; t < T; ++t) m1[t] = bitsf(XK_INF);
+        int bprev = -32;
+        const float c0_key = (float)c0_wave * LR_C0_EPS;  // exact
+
+        for (int k = 0; k < nchunks; ++k) {
+            const int base = k * chunk;
+            const int ncols = min(chunk, cols - base);
+            if (k || pass) __syncthreads();
+            // expand the chunk's right descriptors, the digit constants in the last step
+            for (int c = threadIdx.x; c < chunk; c += blockDim.x) {
+                const int c1 = base + c;
+#pragma unroll
+                for (int w = 0; w < WL; ++w) {
+                    v4i v;
+                    if (w == WL - 1) {
+                        v = fk_digits(c1 & 31);
+                        v[1] = (int)((uint32_t)v[1] | LR_A_W1);
+                    } else {
+                        const uint32_t x = c1 < cols ? row1[(size_t)c1 * WORDS + w] : 0u;
+                        v = expand_bits(x, LUT_A);
+                        if (w == WL - 2) {
+                            v[1] = (int)((uint32_t)v[1] | LR_A_ABS1);
+                            v[2] = (int)((uint32_t)v[2] | LR_A_ABS23);
+                            v[3] = (int)((uint32_t)v[3] | LR_A_ABS23);
+                        }
+                    }
+                    lds_mx[w * chunk + c] = v;
+                }
+            }
+            __syncthreads();
+            if (idle) continue;
+
+            const int nfull = ncols / 32;
+            const bool partial = (ncols & 31) != 0;
+            auto block = [&](int b, const v16f& cb) {
+                const int B = base + 32 * b;
+                v4i af[KS];
+#pragma unroll
+                for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + 32 * b + j];
+                v16f d[T];
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    if constexpr (KS == 1) {
+                        d[t] = mfma_fp4_sa(af[0], bf[t][0], cb, sa_hi);
+                    } else {
+                        d[t] = mfma_fp4(af[0], bf[t][0], cb);
+#pragma unroll
+                        for (int s = 1; s < KS; ++s)
+                            d[t] = s == KS - 1 ? mfma_fp4_sa(af[s], bf[t][s], d[t], sa_hi)
+                                               : mfma_fp4(af[s], bf[t][s], d[t]);
+                    }
+                }
+#pragma unroll
+                for (int t = 0; t < T; ++t) m1[t] = fmin16(d[t], m1[t] - 32.f * FK_EPS);
+                uint32_t v[16];
+#pragma unroll
+                for (int r = 0; r < 16; ++r) v[r] = min(fbits(d[0][r]), fbits(d[1][r]));
+                const uint32_t y = fbits(bitsf(lr_reduce(v, lane)) + c0_key);
+                if ((lane & 1) == 0) atomicMin(&rev[B + rc1], y);
+                bprev = B;
+            };
+            v16f cz;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) cz[r] = 0.f;  // C = 0: an inline constant
+            for (int b = 0; b < nfull; ++b) block(b, cz);
+            if (partial) {
+                v16f cp;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) cp[r] = 32 * nfull + rrow(r) < ncols ? 0.f : KEY_PAD;
+                block(nfull, cp);
+            }
+        }
+        // this pass's forward results: both lane halves' minima; half h writes tile h
+#pragma unroll
+        for (int t = 0; t < T; ++t)
+            m1[t] = __builtin_fminf(m1[t], bitsf((uint32_t)__shfl_xor((int)fbits(m1[t]), 32)));
+        const int c0 = c0_wave + 2 * j + h;
+        if (!idle && c0 < cols) {
+            const float v = (h ? m1[1] : m1[0]) - (float)(2 * j + h) * LR_C0_EPS;  // exact
+            fwd[c0] = (int16_t)(bprev + (int)((v - __builtin_rintf(v)) * 4096.f));
+        }
+    }
+    __syncthreads();
+    // the left-right check (bicos.hpp:99-106): rev's key of fwd[col0] holds the reverse
+    // search's first col0 at the minimum: bits of D * 2^15 = ham 2^15 + 8 (col1 % 32) + col0
+    int16_t* out = a.out + (size_t)row * a.out_pitch;
+    for (int c0 = threadIdx.x; c0 < cols; c0 += blockDim.x) {
+        const int c1 = fwd[c0];
+        const uint32_t kq = (uint32_t)(bitsf(rev[c1]) * 32768.f);  // exact integer
+        const int r0 = (int)(kq & 0x7FFFu) - 8 * (c1 & 31);
+        const int dlr = c0 - r0;
+        out[c0] = (dlr <= max_lr_diff && -dlr <= max_lr_diff) ? (int16_t)((c0 + r0) / 2 - c1)
+                                                               : INVALID_I16;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
 // Packed Hamming keys (NoDuplicates, descriptors with <= 127 used bits, 32/64/128-bit words).
 //
 // The search above spends most of its VALU issue on the first-minimum trees: one v_min3_u32
@@ -1713,6 +1987,34 @@ hipError_t launch_search_mx_agree(SearchArgs a, const AgreeArgs& ag, const MxGeo
     if (g.T == 2)
         return launch_mx_grid<4, 2, true, 2, 2, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st, &ag);
     return launch_mx_grid<4, 2, true, 4, 2, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st, &ag);
+}
+
+bool search_lr_eligible(int words, int bits, int cols) {
+    return words == 8 && bits > 128 && bits <= 3 * 64 - LR_FREE_BITS && cols >= 1 &&
+           cols <= LR_MAX_COLS;
+}
+
+hipError_t launch_search_lr(SearchArgs a, int words, int bits, int max_lr_diff, hipStream_t st) {
+    if (a.rows <= 0 || a.cols <= 0) return hipSuccess;
+    if (!search_lr_eligible(words, bits, a.cols) || a.keep || a.out_mode != 0)
+        return hipErrorInvalidValue;
+    constexpr int KS = 3, WL = 2 * KS;
+    // 8 waves of 2 x 32 col0 per pass (fewer for narrow rows); the LDS stage as the KEYS 3
+    // search's (64 KiB) plus the row's reverse keys and forward results
+    const int waves = std::min(8, (a.cols + 63) / 64);
+    const int cols32 = (a.cols + 31) & ~31;
+    int chunk = (64 * 1024 / (WL * 16)) & ~31;
+    if (chunk > cols32) chunk = cols32;
+    a.chunk = chunk;
+    const size_t lds = (size_t)WL * chunk * 16 + (size_t)cols32 * 6;
+    const auto kern = search_lr_kernel<8, KS>;
+    if (lds > 64 * 1024) {
+        const hipError_t e = hipFuncSetAttribute((const void*)kern,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(kern, dim3(a.rows), dim3(64 * waves), lds, st, a, max_lr_diff);
+    return hipGetLastError();
 }
 
 hipError_t launch_search_mx(SearchArgs a, const MxGeometry& g, int words, bool nodupes,

@@ -1334,8 +1334,9 @@ def test_search_agree_entry_equals_match(gpu, n, H, W, dt, kw):
     (33, 4, 1032, np.uint8, dict(nxcorr_threshold=0.9, variant=1, max_lr_diff=3)),
     (65, 3, 260, np.uint8, dict(nxcorr_threshold=0.2, variant=1, max_lr_diff=1)),
 ])
-def test_consistency_in_agree(gpu, oracle, n, H, W, dt, kw):
+def test_consistency_in_agree(gpu, oracle, monkeypatch, n, H, W, dt, kw):
     from libbicos_amd.device import MatchConfig
+    monkeypatch.setenv("BICOS_LR_ONE_PASS", "0")  # (n = 40 first minimum: the one-pass form)
     L, R = stereo_stack(n, H, W, dt, dmin=2, drange=50, seed=n * 7 + W)
     L[:, 1, 40:90] = 5  # flat patch: NaN correlations pass
     s0, s1 = dev(L), dev(R)
@@ -1372,8 +1373,9 @@ def test_consistency_in_agree(gpu, oracle, n, H, W, dt, kw):
     (17, 640, dict(variant=1, max_lr_diff=3)),
 ])
 @pytest.mark.parametrize("nxc", [None, 0.8])
-def test_consistency_dense_rows(gpu, oracle, n, W, kw, nxc):
+def test_consistency_dense_rows(gpu, oracle, monkeypatch, n, W, kw, nxc):
     from libbicos_amd.device import MatchConfig
+    monkeypatch.setenv("BICOS_LR_ONE_PASS", "0")  # (n = 40 first minimum: the one-pass form)
     H = 12
     L, R = stereo_stack(n, H, W, dmin=2, drange=40, seed=n + W)
     Rr = random_stack(n, H, W, seed=n * W)
@@ -1388,6 +1390,86 @@ def test_consistency_dense_rows(gpu, oracle, n, W, kw, nxc):
     same(host(d), rd)
     if rc is not None:
         same(host(c), rc)
+
+
+# ------------------------------- Consistency in one pass (search_mx.hip search_lr_kernel)
+# First-minimum Consistency over 256-bit descriptors with 129..154 used bits and <= 2048
+# columns: both searches from one set of matrix products and the left-right check in the same
+# workgroup. Descriptor level (bicos_search_device with the used-bits hint) on random,
+# shifted-copy and low-entropy descriptors (ties everywhere, both directions' first minimum),
+# all-zero / all-one columns (|a| = 0 / bits), every width class of the pass split, against
+# the oracle and against the two-launch form (BICOS_LR_ONE_PASS=0).
+def _lr_desc(H, W, bits, seed, kind):
+    rng = np.random.default_rng(seed)
+    d = rng.integers(0, 2 ** 32, size=(H, W, 8), dtype=np.uint64).astype(np.uint32)
+    if kind == "low":
+        d[...] = 0
+        d[..., 0] = rng.integers(0, 16, size=(H, W), dtype=np.uint32)
+        d[..., 4] = np.where(rng.random((H, W)) < 0.5, np.uint32(0x3FFFFFF), np.uint32(0))
+    d = _lr_mask(d, bits)
+    if kind != "low" and W > 4:  # |a| = 0 and |a| = bits
+        d[0, 1] = 0
+        d[0, 3] = _lr_mask(np.full(8, 0xFFFFFFFF, np.uint32), bits)
+    return d
+
+
+@pytest.mark.parametrize("W", [1, 31, 65, 333, 700, 1030, 2048])
+@pytest.mark.parametrize("bits", [129, 154])
+def test_search_lr_one_pass(gpu, oracle, monkeypatch, W, bits):
+    H = 3
+    rng = np.random.default_rng(W + bits)
+    for kind in ("random", "shifted", "low"):
+        a = _lr_desc(H, W, bits, W * 3 + bits, kind)
+        if kind == "shifted":  # a stereo-like match 5 columns away, 3 % of the words off by one bit
+            flip = (rng.random((H, W, 8)) < 0.03).astype(np.uint32) << rng.integers(0, 32, (H, W, 8)).astype(np.uint32)
+            b = _lr_mask(a[:, np.roll(np.arange(W), 5)] ^ flip, bits)
+        else:
+            b = _lr_desc(H, W, bits, W * 5 + bits + 1, kind)
+        for lr in (0, 1, 4):
+            ref = oracle.search(a, b, 2, lr)
+            monkeypatch.delenv("BICOS_LR_ONE_PASS", raising=False)
+            out = host(gpu.search(dev(_pack(a)), dev(_pack(b)), W, 8, 2, lr, bits=bits))
+            same(out, ref)
+            monkeypatch.setenv("BICOS_LR_ONE_PASS", "0")
+            two = host(gpu.search(dev(_pack(a)), dev(_pack(b)), W, 8, 2, lr, bits=bits))
+            same(two, ref)
+
+
+def _lr_mask(d, bits):
+    full = np.zeros(8, np.uint32)
+    for b in range(bits):
+        full[b // 32] |= np.uint32(1 << (b % 32))
+    return d & full
+
+
+# the match: LIMITED n = 34..40 and FULL n = 13 (146 bits), u8 / u16, with and without NXC,
+# min-variance, a subpixel step (the one-pass map feeds the subpixel refine), flat patches
+@pytest.mark.parametrize("n,H,W,dt,kw", [
+    (40, 6, 2048, np.uint8, dict(nxcorr_threshold=0.96, variant=1, max_lr_diff=1)),
+    (40, 5, 1300, np.uint8, dict(nxcorr_threshold=None, variant=1, max_lr_diff=0)),
+    (34, 4, 700, np.uint16, dict(nxcorr_threshold=0.8, variant=1, max_lr_diff=3, min_variance=1.0)),
+    (37, 4, 333, np.uint8, dict(nxcorr_threshold=0.9, variant=1, max_lr_diff=2, subpixel_step=0.25)),
+    (13, 4, 517, np.uint8, dict(nxcorr_threshold=0.5, variant=1, max_lr_diff=1, mode=1)),
+])
+def test_consistency_one_pass(gpu, oracle, monkeypatch, n, H, W, dt, kw):
+    from libbicos_amd.device import MatchConfig
+    L, R = stereo_stack(n, H, W, dt, dmin=2, drange=50, seed=n * 11 + W)
+    L[:, 1, 40:90] = 5  # flat patch: every distance ties
+    R[:, 1, 30:95] = 5
+    s0, s1 = dev(L), dev(R)
+    cfg = MatchConfig(**kw)
+    monkeypatch.delenv("BICOS_LR_ONE_PASS", raising=False)
+    assert gpu.plan(s0, s1, cfg) & _lib.PLAN_CONSISTENCY_ONE_PASS
+    d, c = gpu.match(s0, s1, cfg)
+    rd, rc = oracle.match(L, R, oracle.OracleConfig(**kw))
+    same(host(d), rd)
+    if rc is not None:
+        same(host(c), rc)
+    assert not gpu.plan(s0, s1, MatchConfig(**dict(kw, no_dupes=True))) & _lib.PLAN_CONSISTENCY_ONE_PASS
+    monkeypatch.setenv("BICOS_LR_ONE_PASS", "0")
+    assert not gpu.plan(s0, s1, cfg) & _lib.PLAN_CONSISTENCY_ONE_PASS
+    d2, c2 = gpu.match(s0, s1, cfg)
+    same(host(d2), host(d))
 
 
 # ------------------ the 128-bit packed-key search with its fused agree (variant 68 / BICOS_PK128=1)
