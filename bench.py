@@ -255,16 +255,21 @@ def mx_key_pair_peak(words: int, cfg: dict, reach: float = MX_REACH_PLANTED) -> 
     return 1024.0 / per_unit_s
 
 
-def lr_key_pair_peak() -> float:
+def lr_key_pair_peak(tiles: int = 4) -> float:
     """Issue bound in pairs/s of the one-pass Consistency search's VALU (search_mx.hip
-    search_lr_kernel), from its ISA per wave and block of 2 tiles x 32 col1 =
-    2048 pairs: forward 16 v_min3_f32 (half rate) + 2 v_add_f32; reverse 16 v_min_u32 (the tile
-    pair), 8 v_permlane16_swap + 8 v_min_u32, 7 v_min_u32_dpp + 1 v_min_u32 (half), 14
-    v_cndmask + v_mov_dpp + v_add_f32 (full), 4 LDS-address v_add_u32 (full): 56 half-rate and
-    22 full-rate lane-ops per lane."""
-    half = 56.0 * 64 / 2048
-    full = 22.0 * 64 / 2048
-    return 1.0 / (half / (VALU_HALF_TOPS * 1e12) + full / (VALU_FULL_TOPS * 1e12))
+    search_lr_kernel), from its ISA per wave and block of `tiles` x 32 col0 x
+    32 col1 pairs: forward 8 v_min3_f32 (half rate) + 1 v_sub_f32 per tile; the reverse keys'
+    minimum over the tiles (16 v_min_u32, then 16 v_min3_u32 per further pair: half); the lane
+    transposition (8 v_permlane16_swap at a quarter rate, 8 + 7 DPP + 1 v_min_u32: half; 14
+    v_cndmask, a v_mov_dpp, a v_add_f32: full) and ~6 address / exec VALU (full). T = 4 (the
+    default): 96 half-rate and 26 full-rate instructions per 4096 pairs; T = 2 (BICOS_LR_T=2):
+    56 and 22 per 2048."""
+    if tiles == 2:
+        half, full, pairs = 56.0, 22.0, 2048.0
+    else:
+        half, full, pairs = 96.0, 26.0, 4096.0
+    per_pair_s = half * 64 / pairs / (VALU_HALF_TOPS * 1e12) + full * 64 / pairs / (VALU_FULL_TOPS * 1e12)
+    return 1.0 / per_pair_s
 
 
 def mx_key_pair_peak_all_trees() -> float:
@@ -1241,7 +1246,8 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
                                      mark[:, :W].sum(dim=1)).sum().item())
     if mx:
         alg_flops, used_flops = mx_flops(rows, W, words, mc, ubits, sbits, reverse_col1=kept)
-        kpeak = (lr_key_pair_peak() if one_pass else pk_key_pair_peak() if pk else
+        kpeak = (lr_key_pair_peak(2 if os.environ.get("BICOS_LR_T") == "2" else 4) if one_pass else
+                 pk_key_pair_peak() if pk else
                  mx_key_pair_peak(words, mc, mx_reach_planted(W))) / 1e9
         evaluated = pairs + (kept if kept is not None else pairs / W) * W if cons else pairs
         k_exec = int(round(alg_flops / (2 * evaluated)))
@@ -1295,8 +1301,8 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
                 "key_reduction_ms": round(t_key * 1e3, 4),
                 "agree_hbm_ms": round(t_ag * 1e3, 4),
                 "bound_ms": round(t_bound * 1e3, 4),
-                "key_model": ("lr_key_pair_peak: 56 half-rate + 22 full-rate lane-ops per lane and "
-                              "block of 2 tiles (both directions' reductions)" if one_pass else
+                "key_model": ("lr_key_pair_peak: 96 half-rate + 26 full-rate instructions per wave "
+                              "and block of 4 tiles (both directions' reductions)" if one_pass else
                               "pk_key_pair_peak: 10 half-rate + 1 full-rate lane-ops per lane, wide "
                               "tile and block" if pk else
                               "mx_key_pair_peak: the ISA's VALU per (wave, tile, block), the "
@@ -1328,6 +1334,16 @@ def kernel_roofline(args, C, torch, dev, eng, mcfg, s0, s1, rows, W, n, words, w
             },
             "key_reduction_view": dict(kview, what="the VALU key reduction as executed (issue bound "
                                                    "at the measured rates), alone"),
+            # gfx950 runs the MFMAs and the VALU of the waves sharing a SIMD one after the other
+            # (profiles/mfma_valu_overlap_r06.jsonl: an MFMA wave + a VALU wave on one SIMD take
+            # the SUM of their times, FP4 and bf16 alike), so the launch's floor is the sum
+            "serial_view": {
+                "ms": round((t_fp4 + t_key + t_ag) * 1e3, 4),
+                "frac": round((t_fp4 + t_key + t_ag) / t_main, 4),
+                "what": "FP4 floor + key reduction as executed%s, added: the matrix pipe and the "
+                        "VALU of one SIMD serialize (tools/mfma_valu_overlap.hip, "
+                        "profiles/mfma_valu_overlap_r06.jsonl)" % (" + agree bytes" if fused else ""),
+            },
             "all_trees_view": None if pk else {
                 "peak": round(mx_key_pair_peak_all_trees() / 1e9, 1),
                 "frac": round(evaluated / mx_key_pair_peak_all_trees() / t_main, 4),

@@ -985,21 +985,21 @@ void search_mx_kernel(typename SearchKArgs<AG>::type ka) {
 //    lower half (descriptor bits 26..31 of word 2 KS - 2, zero for <= 64 KS - 38 used bits):
 //    right (A) constants 1, 6, 6, 6, 6, 6, left (B) FP4 digits with sum = |a| (lr_abs_digits);
 //  * col1 % 32 as KEYS 3 (fk_digits in the upper half's A, B = 2.0, the half scaled 2^-13);
-//  * col0 - c0_wave = 2 j + t in 6 more upper-half elements: A constants 0.5, 0.5, 0.5, 0.5, 1,
-//    2, B = bit k ? 0.5, 1, 2, 4, 4, 4 : 0 (products 2^-2 .. 2^3, x 2^-13).
+//  * col0 - c0_wave = T j + t in 7 more upper-half elements: A constants 0.5, 0.5, 0.5, 0.5, 1,
+//    2, 4, B = bit k ? 0.5, 1, 2, 4, 4, 4, 4 : 0 (products 2^-2 .. 2^4, x 2^-13).
 // Forward: col0 fixed, so D orders by ham, then col1 (the first minimum); the running minimum
 // is kept relative to the block base exactly as KEYS 3. Reverse: col1 fixed, so D orders by
-// ham, then col0: the tile pair's v_min, the lane transposition, + c0_wave * 2^-15 (exact), and
+// ham, then col0: the tiles' v_min / v_min3, the lane transposition, + c0_wave * 2^-15, and
 // one ds_min_u32 per col1 into the row's LDS array (D >= 0: the bits order like the float).
 // Left columns past the image carry |a| digits of 186 > any distance, so they never win.
-// col0 of wave w in pass p: c0_wave + 2 j + t, c0_wave = (p waves + w) * 64 (interleaved, so
-// the 6-bit col0 offset is the lane and the tile). Passes cover the row; the right row is
+// col0 of wave w in pass p: c0_wave + T j + t, c0_wave = (p waves + w) * 32 T (interleaved, so
+// the col0 offset is the lane and the tile). Passes cover the row; the right row is
 // re-expanded per pass (~2 % of the VALU). The epilogue reads fwd[col0] and rev[fwd[col0]]
 // from LDS and writes consistency_kernel's disparity (reference bicos.hpp:99-106).
 constexpr int LR_MAX_COLS = FK_MAX_COLS;
 constexpr int LR_SA_HI = 127 - 13;              // E8M0 2^-13: the upper half of the last step
 constexpr float LR_C0_EPS = 1.f / 32768.f;      // col0 * 2^-15
-constexpr uint32_t LR_A_W1 = 0x04211110u;       // col0 digit constants, nibbles 1..6 of dword 1
+constexpr uint32_t LR_A_W1 = 0x64211110u;       // col0 digit constants, nibbles 1..7 of dword 1
 constexpr uint32_t LR_B_W0 = 0x44444444u;       // 2.0 against the col1 digits (dword 0 ...
 constexpr uint32_t LR_B_W1 = 0x4u;              // ... and nibble 0 of dword 1)
 constexpr uint32_t LR_A_ABS1 = 0x72000000u;     // |a| constants 1, 6 (top byte of dword 1)
@@ -1069,10 +1069,10 @@ __device__ __forceinline__ uint32_t lr_reduce(const uint32_t (&v)[16], int lane)
     return min(y, lr_mov<0xB1>(y));             // quad_perm [1, 0, 3, 2]
 }
 
-template <int WORDS, int KS>
+template <int WORDS, int KS, int T>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4)))
 void search_lr_kernel(SearchArgs a, int max_lr_diff) {
-    constexpr int T = 2;
+    static_assert(T == 2 || T == 4, "tiles in pairs, <= 128 col0 per wave (7 digit bits)");
     constexpr int WL = 2 * KS;
     static_assert(2 * KS <= WORDS, "K-steps exceed the descriptor");
     extern __shared__ __attribute__((aligned(16))) v4i lds_mx[];  // [WL][chunk] | rev | fwd
@@ -1113,7 +1113,7 @@ void search_lr_kernel(SearchArgs a, int max_lr_diff) {
         v4i bf[T][KS];
 #pragma unroll
         for (int t = 0; t < T; ++t) {
-            const int c0 = c0_wave + 2 * j + t;
+            const int c0 = c0_wave + T * j + t;
             const bool in = c0 < cols;
             int pc = 0;
 #pragma unroll
@@ -1132,11 +1132,11 @@ void search_lr_kernel(SearchArgs a, int max_lr_diff) {
                 f[2] = (int)(((uint32_t)f[2] & 0x00FFFFFFu) | (b2 << 24));
                 f[3] = (int)(((uint32_t)f[3] & 0x00FFFFFFu) | (b3 << 24));
             } else {
-                const uint32_t c0w = (uint32_t)(2 * j + t);
+                const uint32_t c0w = (uint32_t)(T * j + t);
                 uint32_t w1 = LR_B_W1;
-                constexpr uint32_t code[6] = {0x1u, 0x2u, 0x4u, 0x6u, 0x6u, 0x6u};
+                constexpr uint32_t code[7] = {0x1u, 0x2u, 0x4u, 0x6u, 0x6u, 0x6u, 0x6u};
 #pragma unroll
-                for (int k = 0; k < 6; ++k)
+                for (int k = 0; k < 7; ++k)
                     if (c0w & (1u << k)) w1 |= code[k] << (4 * (k + 1));
                 bf[t][KS - 1] = v4i{(int)LR_B_W0, (int)w1, 0, 0};
             }
@@ -1180,26 +1180,41 @@ void search_lr_kernel(SearchArgs a, int max_lr_diff) {
             auto block = [&](int b, const v16f& cb) {
                 const int B = base + 32 * b;
                 v4i af[KS];
+                // the A fragments, read again for every tile pair (T = 4: not held across the
+                // first pair's key reduction -- 12 registers)
+                auto load_af = [&](int p) {
+                    int o = 32 * b + j;
+                    if (p) asm volatile("" : "+v"(o));  // (a second read, not a copy)
 #pragma unroll
-                for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + 32 * b + j];
-                v16f d[T];
-#pragma unroll
-                for (int t = 0; t < T; ++t) {
+                    for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + o];
+                };
+                auto products = [&](int t) {
+                    v16f d;
                     if constexpr (KS == 1) {
-                        d[t] = mfma_fp4_sa(af[0], bf[t][0], cb, sa_hi);
+                        d = mfma_fp4_sa(af[0], bf[t][0], cb, sa_hi);
                     } else {
-                        d[t] = mfma_fp4(af[0], bf[t][0], cb);
+                        d = mfma_fp4(af[0], bf[t][0], cb);
 #pragma unroll
                         for (int s = 1; s < KS; ++s)
-                            d[t] = s == KS - 1 ? mfma_fp4_sa(af[s], bf[t][s], d[t], sa_hi)
-                                               : mfma_fp4(af[s], bf[t][s], d[t]);
+                            d = s == KS - 1 ? mfma_fp4_sa(af[s], bf[t][s], d, sa_hi)
+                                            : mfma_fp4(af[s], bf[t][s], d);
                     }
-                }
-#pragma unroll
-                for (int t = 0; t < T; ++t) m1[t] = fmin16(d[t], m1[t] - 32.f * FK_EPS);
+                    return d;
+                };
+                // tiles in pairs: the forward trees, and the reverse keys' minimum over the
+                // tiles (v_min for the first pair, v_min3 after)
                 uint32_t v[16];
 #pragma unroll
-                for (int r = 0; r < 16; ++r) v[r] = min(fbits(d[0][r]), fbits(d[1][r]));
+                for (int p = 0; p < T / 2; ++p) {
+                    load_af(p);
+                    const v16f d0 = products(2 * p), d1 = products(2 * p + 1);
+                    m1[2 * p] = fmin16(d0, m1[2 * p] - 32.f * FK_EPS);
+                    m1[2 * p + 1] = fmin16(d1, m1[2 * p + 1] - 32.f * FK_EPS);
+#pragma unroll
+                    for (int r = 0; r < 16; ++r)
+                        v[r] = p == 0 ? min(fbits(d0[r]), fbits(d1[r]))
+                                      : umin3(v[r], fbits(d0[r]), fbits(d1[r]));
+                }
                 const uint32_t y = fbits(bitsf(lr_reduce(v, lane)) + c0_key);
                 if ((lane & 1) == 0) atomicMin(&rev[B + rc1], y);
                 bprev = B;
@@ -1215,14 +1230,16 @@ void search_lr_kernel(SearchArgs a, int max_lr_diff) {
                 block(nfull, cp);
             }
         }
-        // this pass's forward results: both lane halves' minima; half h writes tile h
+        // this pass's forward results: both lane halves' minima; half h writes the tiles t
+        // with t % 2 == h
 #pragma unroll
-        for (int t = 0; t < T; ++t)
+        for (int t = 0; t < T; ++t) {
             m1[t] = __builtin_fminf(m1[t], bitsf((uint32_t)__shfl_xor((int)fbits(m1[t]), 32)));
-        const int c0 = c0_wave + 2 * j + h;
-        if (!idle && c0 < cols) {
-            const float v = (h ? m1[1] : m1[0]) - (float)(2 * j + h) * LR_C0_EPS;  // exact
-            fwd[c0] = (int16_t)(bprev + (int)((v - __builtin_rintf(v)) * 4096.f));
+            const int c0 = c0_wave + T * j + t;
+            if ((t & 1) == h && !idle && c0 < cols) {
+                const float v = m1[t] - (float)(T * j + t) * LR_C0_EPS;  // exact
+                fwd[c0] = (int16_t)(bprev + (int)((v - __builtin_rintf(v)) * 4096.f));
+            }
         }
     }
     __syncthreads();
@@ -1989,6 +2006,12 @@ hipError_t launch_search_mx_agree(SearchArgs a, const AgreeArgs& ag, const MxGeo
     return launch_mx_grid<4, 2, true, 4, 2, false, false, true>(a, g.waves, a.rows * a.tiles_per_row, st, &ag);
 }
 
+// tiles per wave of the one-pass Consistency search (BICOS_LR_T=2: two, A/B)
+static int lr_tiles() {
+    const char* v = std::getenv("BICOS_LR_T");
+    return v && std::atoi(v) == 2 ? 2 : 4;
+}
+
 bool search_lr_eligible(int words, int bits, int cols) {
     return words == 8 && bits > 128 && bits <= 3 * 64 - LR_FREE_BITS && cols >= 1 &&
            cols <= LR_MAX_COLS;
@@ -2001,13 +2024,13 @@ hipError_t launch_search_lr(SearchArgs a, int words, int bits, int max_lr_diff, 
     constexpr int KS = 3, WL = 2 * KS;
     // 8 waves of 2 x 32 col0 per pass (fewer for narrow rows); the LDS stage as the KEYS 3
     // search's (64 KiB) plus the row's reverse keys and forward results
-    const int waves = std::min(8, (a.cols + 63) / 64);
+    const int waves = std::min(8, (a.cols + 32 * lr_tiles() - 1) / (32 * lr_tiles()));
     const int cols32 = (a.cols + 31) & ~31;
     int chunk = (64 * 1024 / (WL * 16)) & ~31;
     if (chunk > cols32) chunk = cols32;
     a.chunk = chunk;
     const size_t lds = (size_t)WL * chunk * 16 + (size_t)cols32 * 6;
-    const auto kern = search_lr_kernel<8, KS>;
+    const auto kern = lr_tiles() == 4 ? search_lr_kernel<8, KS, 4> : search_lr_kernel<8, KS, 2>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
