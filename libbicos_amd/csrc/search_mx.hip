@@ -1177,7 +1177,11 @@ void search_lr_kernel(SearchArgs a, int max_lr_diff) {
 
             const int nfull = ncols / 32;
             const bool partial = (ncols & 31) != 0;
-            auto block = [&](int b, const v16f& cb) {
+            // PART: the block reaching past the image (last chunk); its rows past it are set to
+            // KEY_PAD after the products (16 v_cndmask per tile in that block only), so every
+            // block runs with C = 0 (a C matrix for it made the 4-tile kernel spill)
+            auto block = [&](int b, auto part_tag) {
+                constexpr bool PART = decltype(part_tag)::value;
                 const int B = base + 32 * b;
                 v4i af[KS];
                 // the A fragments, read again for every tile pair (T = 4: not held across the
@@ -1191,13 +1195,18 @@ void search_lr_kernel(SearchArgs a, int max_lr_diff) {
                 auto products = [&](int t) {
                     v16f d;
                     if constexpr (KS == 1) {
-                        d = mfma_fp4_sa(af[0], bf[t][0], cb, sa_hi);
+                        d = mfma_fp4_sa(af[0], bf[t][0], v16f{}, sa_hi);
                     } else {
-                        d = mfma_fp4(af[0], bf[t][0], cb);
+                        d = mfma_fp4(af[0], bf[t][0], v16f{});
 #pragma unroll
                         for (int s = 1; s < KS; ++s)
                             d = s == KS - 1 ? mfma_fp4_sa(af[s], bf[t][s], d, sa_hi)
                                             : mfma_fp4(af[s], bf[t][s], d);
+                    }
+                    if constexpr (PART) {
+#pragma unroll
+                        for (int r = 0; r < 16; ++r)
+                            if (32 * b + rrow(r) >= ncols) d[r] = KEY_PAD;
                     }
                     return d;
                 };
@@ -1219,16 +1228,8 @@ void search_lr_kernel(SearchArgs a, int max_lr_diff) {
                 if ((lane & 1) == 0) atomicMin(&rev[B + rc1], y);
                 bprev = B;
             };
-            v16f cz;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) cz[r] = 0.f;  // C = 0: an inline constant
-            for (int b = 0; b < nfull; ++b) block(b, cz);
-            if (partial) {
-                v16f cp;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) cp[r] = 32 * nfull + rrow(r) < ncols ? 0.f : KEY_PAD;
-                block(nfull, cp);
-            }
+            for (int b = 0; b < nfull; ++b) block(b, std::false_type{});
+            if (partial) block(nfull, std::true_type{});
         }
         // this pass's forward results: both lane halves' minima; half h writes the tiles t
         // with t % 2 == h
