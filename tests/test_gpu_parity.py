@@ -1447,6 +1447,8 @@ def _lr_mask(d, bits):
 @pytest.mark.parametrize("n,H,W,dt,kw", [
     (40, 6, 2048, np.uint8, dict(nxcorr_threshold=0.96, variant=1, max_lr_diff=1)),
     (40, 5, 1300, np.uint8, dict(nxcorr_threshold=None, variant=1, max_lr_diff=0)),
+    (40, 7, 1000, np.uint8, dict(nxcorr_threshold=0.5, variant=1, max_lr_diff=2, min_variance=1.0)),
+    (40, 3, 77, np.uint8, dict(nxcorr_threshold=0.0, variant=1, max_lr_diff=0)),
     (34, 4, 700, np.uint16, dict(nxcorr_threshold=0.8, variant=1, max_lr_diff=3, min_variance=1.0)),
     (37, 4, 333, np.uint8, dict(nxcorr_threshold=0.9, variant=1, max_lr_diff=2, subpixel_step=0.25)),
     (13, 4, 517, np.uint8, dict(nxcorr_threshold=0.5, variant=1, max_lr_diff=1, mode=1)),
@@ -1459,7 +1461,8 @@ def test_consistency_one_pass(gpu, oracle, monkeypatch, n, H, W, dt, kw):
     s0, s1 = dev(L), dev(R)
     cfg = MatchConfig(**kw)
     monkeypatch.delenv("BICOS_LR_ONE_PASS", raising=False)
-    assert gpu.plan(s0, s1, cfg) & _lib.PLAN_CONSISTENCY_ONE_PASS
+    plan = gpu.plan(s0, s1, cfg)
+    assert plan & _lib.PLAN_CONSISTENCY_ONE_PASS and not plan & _lib.PLAN_AGREE_IN_SEARCH
     d, c = gpu.match(s0, s1, cfg)
     rd, rc = oracle.match(L, R, oracle.OracleConfig(**kw))
     same(host(d), rd)
@@ -1470,6 +1473,8 @@ def test_consistency_one_pass(gpu, oracle, monkeypatch, n, H, W, dt, kw):
     assert not gpu.plan(s0, s1, cfg) & _lib.PLAN_CONSISTENCY_ONE_PASS
     d2, c2 = gpu.match(s0, s1, cfg)
     same(host(d2), host(d))
+    if c is not None:
+        same(host(c2), host(c))
 
 
 # ------------------ the 128-bit packed-key search with its fused agree (variant 68 / BICOS_PK128=1)
