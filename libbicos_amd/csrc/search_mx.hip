@@ -1005,6 +1005,10 @@ constexpr uint32_t LR_B_W1 = 0x4u;              // ... and nibble 0 of dword 1)
 constexpr uint32_t LR_A_ABS1 = 0x72000000u;     // |a| constants 1, 6 (top byte of dword 1)
 constexpr uint32_t LR_A_ABS23 = 0x77000000u;    // 6, 6 (dwords 2 and 3)
 constexpr int LR_FREE_BITS = 38;                // 32 upper-half + 6 lower-half K elements
+#ifndef BICOS_LR_BL
+#define BICOS_LR_BL 1
+#endif
+constexpr bool LR_BL = BICOS_LR_BL != 0;         // (see search_lr_kernel)
 
 // FP4 code of u / 2 for u in {0, 1, 2, 3, 4, 6, 8, 12}
 __device__ __forceinline__ uint32_t lr_code(int u) {
@@ -1088,6 +1092,11 @@ void search_lr_kernel(SearchArgs a, int max_lr_diff) {
     const int cols32 = (cols + 31) & ~31;
     uint32_t* rev = reinterpret_cast<uint32_t*>((char*)lds_mx + (size_t)WL * chunk * 16);
     int16_t* fwd = reinterpret_cast<int16_t*>(rev + cols32);
+    // LR_BL: the last K-step's B fragments of the wave's tiles live in LDS (one ds_read_b128 per
+    // tile and block) -- in registers the 4-tile kernel spilled two of them to scratch, whose
+    // reloads per block missed to HBM (PMC: 518 MB read + 129 MB written per cfg4 frame)
+    constexpr bool BL = LR_BL && T == 4;
+    v4i* bfl = reinterpret_cast<v4i*>(fwd + cols32) + (size_t)wave * T * 64;
     for (int i = threadIdx.x; i < cols32; i += blockDim.x) rev[i] = 0xFFFFFFFFu;
 
     const uint32_t* __restrict__ row0 = a.desc0 + (size_t)row * a.desc_pitch;
@@ -1140,6 +1149,7 @@ void search_lr_kernel(SearchArgs a, int max_lr_diff) {
                     if (c0w & (1u << k)) w1 |= code[k] << (4 * (k + 1));
                 bf[t][KS - 1] = v4i{(int)LR_B_W0, (int)w1, 0, 0};
             }
+            if constexpr (BL) bfl[t * 64 + lane] = bf[t][KS - 1];  // (own wave's slots only)
         }
         float m1[T];
 #pragma unroll
@@ -1192,15 +1202,24 @@ void search_lr_kernel(SearchArgs a, int max_lr_diff) {
 #pragma unroll
                     for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + o];
                 };
+                auto b_last = [&](int t) {
+                    if constexpr (BL) {
+                        int o = t * 64 + lane;
+                        asm volatile("" : "+v"(o));  // (read per block, not hoisted into registers)
+                        return bfl[o];
+                    } else {
+                        return bf[t][KS - 1];
+                    }
+                };
                 auto products = [&](int t) {
                     v16f d;
                     if constexpr (KS == 1) {
-                        d = mfma_fp4_sa(af[0], bf[t][0], v16f{}, sa_hi);
+                        d = mfma_fp4_sa(af[0], b_last(t), v16f{}, sa_hi);
                     } else {
                         d = mfma_fp4(af[0], bf[t][0], v16f{});
 #pragma unroll
                         for (int s = 1; s < KS; ++s)
-                            d = s == KS - 1 ? mfma_fp4_sa(af[s], bf[t][s], d, sa_hi)
+                            d = s == KS - 1 ? mfma_fp4_sa(af[s], b_last(t), d, sa_hi)
                                             : mfma_fp4(af[s], bf[t][s], d);
                     }
                     if constexpr (PART) {
@@ -2025,13 +2044,18 @@ hipError_t launch_search_lr(SearchArgs a, int words, int bits, int max_lr_diff, 
     constexpr int KS = 3, WL = 2 * KS;
     // 8 waves of 2 x 32 col0 per pass (fewer for narrow rows); the LDS stage as the KEYS 3
     // search's (64 KiB) plus the row's reverse keys and forward results
-    const int waves = std::min(8, (a.cols + 32 * lr_tiles() - 1) / (32 * lr_tiles()));
+    const int T = lr_tiles();
+    const int waves = std::min(8, (a.cols + 32 * T - 1) / (32 * T));
     const int cols32 = (a.cols + 31) & ~31;
-    int chunk = (64 * 1024 / (WL * 16)) & ~31;
+    // two workgroups per CU: <= 80 KiB each for the stage, the row's keys and results and (4
+    // tiles) the B fragments of the last K-step; cfg4: 384-column chunks
+    const size_t fixed = (size_t)cols32 * 6 + (LR_BL && T == 4 ? (size_t)waves * T * 64 * 16 : 0);
+    int chunk = (int)((80 * 1024 - fixed) / (WL * 16)) & ~31;
     if (chunk > cols32) chunk = cols32;
+    if (chunk < 32) return hipErrorInvalidValue;
     a.chunk = chunk;
-    const size_t lds = (size_t)WL * chunk * 16 + (size_t)cols32 * 6;
-    const auto kern = lr_tiles() == 4 ? search_lr_kernel<8, KS, 4> : search_lr_kernel<8, KS, 2>;
+    const size_t lds = (size_t)WL * chunk * 16 + fixed;
+    const auto kern = T == 4 ? search_lr_kernel<8, KS, 4> : search_lr_kernel<8, KS, 2>;
     if (lds > 64 * 1024) {
         const hipError_t e = hipFuncSetAttribute((const void*)kern,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
