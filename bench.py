@@ -11,8 +11,8 @@ to rank 0 with ONE RCCL gather per step, inside the timed region; the gather of
 step k overlaps the kernels of step k+1 (double-buffered), and every gather has
 completed before the closing barrier.
 
-Frames in flight (--inflight F; on one GPU per config -- 1 for cfg2 / cfg4 / cfg5, 2 for
-cfg1 / cfg3 / readme / integ-* -- and 6 for row bands on N > 1): step k runs on stream k % F with its own
+Frames in flight (--inflight F; on one GPU per config -- 1 for cfg2 / cfg5, 2 for
+cfg1 / cfg3 / cfg4 / readme / integ-* -- and 6 for row bands on N > 1): step k runs on stream k % F with its own
 engine and output buffers, so consecutive frames overlap the way a camera stream is
 processed -- the HBM-bound transform / agree of one frame fill the compute-unit slots the
 previous frame's search leaves idle in its last round of workgroups (narrow row bands:
@@ -122,9 +122,10 @@ del _n, _s, _ms, _cfg
 # keeps 2 only where 2 won by more than the run-to-run spread (~1.3 %): cfg1 (launch-bound:
 # 13030 vs 9729 Mpix/s at F = 1), cfg3 (the subpixel refine overlaps the next frame's search:
 # +2.6 %), readme (+1.9 %) and the integration grid (FULL n = 6 / 8 / 12 / 16 +5.9 / +2.7 /
-# +1.3 / +1.5 %, n = 12 with subpixel +2.2 %). cfg2 / cfg4 / cfg5: F = 1 (cfg2 7740 vs 7668
-# at 20 steps, 7751 vs 7824 at 200; cfg5 4741 vs 4693).
-INFLIGHT_DEFAULT = {"cfg1": 2, "cfg3": 2, "readme": 2}
+# +1.3 / +1.5 %, n = 12 with subpixel +2.2 %). cfg2 / cfg5: F = 1 (cfg2 7740 vs 7668 at 20
+# steps, 7751 vs 7824 at 200; cfg5 4741 vs 4693). cfg4 with the one-launch Consistency search
+# (re-measured): F = 2, 4288 / 4316 vs 4270 / 4267 at 20 steps, 4368 / 4363 vs 4260 / 4278 at 200.
+INFLIGHT_DEFAULT = {"cfg1": 2, "cfg3": 2, "cfg4": 2, "readme": 2}
 
 
 def inflight_default(config: str) -> int:
@@ -383,7 +384,7 @@ def main():
                     help="frames in flight: step k runs on stream k %% F with its own engine, so "
                          "one frame's HBM-bound stages fill the slots the previous frame's "
                          "search leaves idle (1 = strictly one match after another). Default on "
-                         "one GPU: per config (INFLIGHT_DEFAULT: 2 for cfg1 / cfg3 / readme / the "
+                         "one GPU: per config (INFLIGHT_DEFAULT: 2 for cfg1 / cfg3 / cfg4 / readme / the "
                          "integration grid, else 1; "
                          "profiles/inflight_r06.jsonl), 6 for N > 1 row bands and --band-of "
                          "(band 0 of 8: cfg5 0.2140-0.2146 vs 0.2244-0.2281 ms with 3, cfg2 within "
