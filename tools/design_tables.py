@@ -18,9 +18,11 @@ DRIVER_PREV = {"cfg2": " (driver 7718)"}
 
 def bound_text(r):
     bm = r["bound_model"]
-    return "%.3f of its bound (%s: %.4f ms%s); %.3f of dense FP4 alone" % (
+    sv = r.get("serial_view")
+    return "%.3f of its bound (%s: %.4f ms%s); %s%.3f of dense FP4 alone" % (
         r["frac"], r["bound"], bm["bound_ms"],
         " incl. the agree's bytes" if r.get("agree_fused_in_match") else "",
+        "%.3f of FP4 + keys added (`serial_view`, %.4f ms); " % (sv["frac"], sv["ms"]) if sv else "",
         r["fp4_only_view"]["frac"])
 
 
