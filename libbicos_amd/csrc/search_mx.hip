@@ -1202,14 +1202,15 @@ void search_lr_kernel(SearchArgs a, int max_lr_diff) {
 #pragma unroll
                     for (int s = 0; s < KS; ++s) af[s] = lds_mx[(2 * s + h) * chunk + o];
                 };
+                // (one opaque base per block: read per block -- not hoisted into registers --
+                // with the tile in the ds_read's immediate offset)
+                int ob = lane;
+                if constexpr (BL) asm volatile("" : "+v"(ob));
                 auto b_last = [&](int t) {
-                    if constexpr (BL) {
-                        int o = t * 64 + lane;
-                        asm volatile("" : "+v"(o));  // (read per block, not hoisted into registers)
-                        return bfl[o];
-                    } else {
+                    if constexpr (BL)
+                        return bfl[ob + t * 64];
+                    else
                         return bf[t][KS - 1];
-                    }
                 };
                 auto products = [&](int t) {
                     v16f d;
