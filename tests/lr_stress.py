@@ -1,10 +1,12 @@
 """Randomised parity stress of the one-launch Consistency search (search_mx.hip
 search_lr_kernel) against the oracle at the descriptor level: random widths (1..2048), used
 bits (129..154), max_lr_diff (0..6), row counts and descriptor families (random, shifted
-copies with bit flips, low-entropy with heavy ties both ways, few distinct popcounts). One
-JSON line per case to --out; exits non-zero at the first mismatch (its case is the last line).
+copies with bit flips, low-entropy with heavy ties both ways, few distinct popcounts). Test
+infrastructure (it runs the oracle): the GPU suite runs 300 cases (test_lr_stress); run
+directly for more, one JSON line per case to --out, exiting non-zero at the first mismatch
+(its case is the last line):
 
-    python tools/lr_stress.py --cases 300 --out gpurun_out/lr_stress.jsonl
+    python tests/lr_stress.py --cases 4000 --out gpurun_out/lr_stress.jsonl
 """
 import argparse
 import json
@@ -38,22 +40,19 @@ def family(rng, H, W, bits, kind):
     return mask_bits(d, bits)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--cases", type=int, default=200)
-    ap.add_argument("--seed", type=int, default=6)
-    ap.add_argument("--out", default="gpurun_out/lr_stress.jsonl")
-    args = ap.parse_args()
+def run(cases, seed, out):
+    """Returns (number of bit-exact cases, the first mismatching case's record or None)."""
     import torch
     from libbicos_amd.device import Engine
     from oracle import oracle
     from tests.test_gpu_parity import _pack
     eng = Engine(0)
-    rng = np.random.default_rng(args.seed)
-    os.makedirs(os.path.dirname(args.out) or ".", exist_ok=True)
+    rng = np.random.default_rng(seed)
+    if out:
+        os.makedirs(os.path.dirname(out) or ".", exist_ok=True)
     t0 = time.time()
-    with open(args.out, "w") as f:
-        for i in range(args.cases):
+    with open(out or os.devnull, "w") as f:
+        for i in range(cases):
             W = int(rng.choice([1, 2, 31, 32, 33, 63, 64, 65, 127, 128, 129, 383, 384, 385, 511,
                                 512, 513, 1023, 1024, 1025, 1536, 2047, 2048,
                                 int(rng.integers(1, 2049))]))
@@ -71,19 +70,32 @@ def main():
             ref = oracle.search(a, b, 2, lr)
             d0 = torch.from_numpy(_pack(a)).cuda()
             d1 = torch.from_numpy(_pack(b)).cuda()
-            out = eng.search(d0, d1, W, 8, 2, lr, bits=bits).cpu().numpy()
-            ok = bool(np.array_equal(out, ref))
+            res = eng.search(d0, d1, W, 8, 2, lr, bits=bits).cpu().numpy()
+            ok = bool(np.array_equal(res, ref))
             rec = {"case": i, "W": W, "H": H, "bits": bits, "lr": lr, "kind": kind, "ok": ok,
                    "valid": float((ref != -32768).mean())}
             f.write(json.dumps(rec) + "\n")
             f.flush()
             if not ok:
-                bad = np.argwhere(out != ref)[0]
-                print("MISMATCH", rec, "first", bad.tolist(), out[tuple(bad)], ref[tuple(bad)])
-                return 1
-            if i % 25 == 0:
+                bad = np.argwhere(res != ref)[0]
+                rec["first"] = [bad.tolist(), int(res[tuple(bad)]), int(ref[tuple(bad)])]
+                return i, rec
+            if i % 250 == 0:
                 print("case %d ok (%.0f s)" % (i, time.time() - t0), flush=True)
-    print("all %d cases bit-exact (%.0f s)" % (args.cases, time.time() - t0))
+    return cases, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--cases", type=int, default=200)
+    ap.add_argument("--seed", type=int, default=6)
+    ap.add_argument("--out", default="gpurun_out/lr_stress.jsonl")
+    args = ap.parse_args()
+    n, bad = run(args.cases, args.seed, args.out)
+    if bad:
+        print("MISMATCH", bad)
+        return 1
+    print("all %d cases bit-exact" % n)
     return 0
 
 

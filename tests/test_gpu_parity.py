@@ -1502,3 +1502,11 @@ def test_pk128_fused_equals_default(gpu, rows):
     if rows == 192:
         assert band_hashes(host(d), 64) == rec["disparity_bands"][:3]
         assert band_hashes(host(c), 64) == rec["corrmap_bands"][:3]
+
+
+# ------------- the one-launch Consistency search, randomised (tests/lr_stress.py: 300 cases)
+def test_lr_stress(gpu):
+    from tests.lr_stress import run
+    n, bad = run(300, 6, None)
+    assert bad is None, bad
+    assert n == 300
